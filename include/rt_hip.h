@@ -1,0 +1,199 @@
+/*
+ * rt_hip.h — C ABI of the MI355X path-tracing backend (librt_hip.so).
+ *
+ * Drop-in boundary for the per-pixel path-tracing loop of Shinzef/BlenderRayTracer:
+ *   RayTracer.prototype.render(onProgress)            js/ray-tracer.js:166-281
+ *     -> rayColor(ray, depth)                          js/ray-tracer.js:102-123
+ *     -> World.hit / background                        js/world.js:20-110
+ *     -> Sphere/Plane/Box/Triangle/TriangleMesh.hit    js/geometry.js:15-262
+ *     -> Lambertian/Metal/Dielectric/Emissive          js/materials.js:14-96
+ *     -> Camera.getRay                                 js/camera.js:38-51
+ *     -> toneMap / gammaCorrect epilogue               js/ray-tracer.js:151-165, post-processor.js:9-42
+ * The host (JS GpuRayTracer over N-API, or Python over ctypes) packs the reference's duck-typed
+ * World/Camera objects into the plain arrays below; everything under render() runs on the GPU.
+ *
+ * Conventions: plain C types, caller owns every host buffer, the library owns device buffers.
+ * Every int-returning entry point returns 0 on success and a negative rt_status on failure;
+ * rt_last_error() then holds a thread-local message.  No C++ exception crosses this ABI.
+ * Randomness: the keyed counter RNG documented in DESIGN.md §RNG replaces Math.random().
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID = -1,     /* bad argument / descriptor */
+    RT_ERR_DEVICE = -2,      /* HIP runtime error */
+    RT_ERR_NOMEM = -3,
+    RT_ERR_CANCELLED = -4,   /* rt_cancel() was observed between sample batches */
+    RT_ERR_NO_DEVICE = -5    /* no HIP device visible: the backend never falls back to the CPU */
+} rt_status;
+
+/* World object kinds, in the reference's World.objects insertion order (js/world.js:20-33). */
+typedef enum rt_object_type {
+    RT_OBJ_SPHERE = 0,    /* geometry.js:15-45   g = {cx, cy, cz, radius}                     */
+    RT_OBJ_PLANE = 1,     /* geometry.js:56-74   g = {px, py, pz, nx, ny, nz} (n normalized)  */
+    RT_OBJ_BOX = 2,       /* geometry.js:85-132  g = {minx, miny, minz, maxx, maxy, maxz}     */
+    RT_OBJ_TRIANGLE = 3,  /* geometry.js:148-188 one world object = triangles[first]          */
+    RT_OBJ_MESH = 4       /* geometry.js:248-262 triangles[first .. first+count), last tie wins */
+} rt_object_type;
+
+typedef enum rt_material_type {
+    RT_MAT_LAMBERTIAN = 0, /* materials.js:14-26 */
+    RT_MAT_METAL = 1,      /* materials.js:29-42 */
+    RT_MAT_DIELECTRIC = 2, /* materials.js:45-84 */
+    RT_MAT_EMISSIVE = 3    /* materials.js:87-96 */
+} rt_material_type;
+
+typedef enum rt_background_type {
+    RT_BG_GRADIENT = 0,        /* World.skyGradient      world.js:35-40  */
+    RT_BG_SOLID = 1,           /* World.solidBackground  world.js:42-44 (updateBackground form) */
+    RT_BG_HDRI = 2,            /* World.hdriBackground   world.js:74-110 (updateBackground form) */
+    RT_BG_PROCEDURAL_SKY = 3,  /* World.proceduralSky    world.js:46-72  */
+    RT_BG_NAN = 4              /* JSON "solid"/"hdri": the loader binds a factory, radiance is NaN
+                                  (scene-loader.js:41-45) */
+} rt_background_type;
+
+typedef enum rt_camera_type { RT_CAM_PERSPECTIVE = 0, RT_CAM_ORTHOGRAPHIC = 1 } rt_camera_type;
+/* getAntiAliasSample (ray-tracer.js:125-149): any string other than 'stochastic' and
+ * 'supersampling' samples the pixel centre (RT_AA_CENTER) */
+typedef enum rt_aa_mode { RT_AA_SUPERSAMPLING = 0, RT_AA_STOCHASTIC = 1, RT_AA_CENTER = 2 } rt_aa_mode;
+typedef enum rt_tone_map { RT_TM_REINHARD = 0, RT_TM_ACES = 1, RT_TM_LINEAR = 2 } rt_tone_map;
+
+/* Arithmetic of the path kernel.  F64 is the reference's own arithmetic (JS numbers are IEEE
+ * binary64, no FMA contraction): ray paths agree with the reference decision for decision.
+ * F32 is the fast mode; its per-channel RMS vs the reference is measured in tests. */
+typedef enum rt_precision { RT_PREC_F64 = 0, RT_PREC_F32 = 1 } rt_precision;
+
+typedef struct rt_material_desc {
+    int32_t type;          /* rt_material_type */
+    int32_t _pad;
+    double albedo[3];      /* Lambertian / Metal albedo */
+    double roughness;      /* Metal: already Math.min(roughness, 1) (materials.js:33) */
+    double ior;            /* Dielectric refractionIndex */
+    double emission[3];    /* Emissive: color.mul(intensity) (materials.js:95), evaluated in double */
+} rt_material_desc;        /* 80 bytes */
+
+typedef struct rt_object_desc {
+    int32_t type;          /* rt_object_type */
+    int32_t material;      /* index into rt_scene_desc.materials */
+    int32_t first;         /* TRIANGLE / MESH: first triangle */
+    int32_t count;         /* TRIANGLE: 1; MESH: number of triangles (may be 0) */
+    double g[6];           /* geometry, see rt_object_type */
+} rt_object_desc;          /* 64 bytes */
+
+typedef struct rt_camera_desc {  /* vectors exactly as js/camera.js:8-36 computes them */
+    double origin[3];
+    double lower_left[3];
+    double horizontal[3];
+    double vertical[3];
+    double u[3], v[3], w[3];
+    double lens_radius;
+    int32_t type;          /* rt_camera_type ("orthographic" => normalized, focal length 1) */
+    int32_t _pad;
+} rt_camera_desc;
+
+typedef struct rt_scene_desc {
+    int32_t abi_version;                 /* RT_ABI_VERSION */
+    int32_t num_objects;
+    const rt_object_desc* objects;
+    int32_t num_materials;
+    int32_t num_triangles;
+    const rt_material_desc* materials;
+    const double* triangles;             /* 12 doubles each: v0, v1, v2, unit geometric normal
+                                            normalize(cross(v1-v0, v2-v0)) (geometry.js:143-145) */
+    rt_camera_desc camera;
+    int32_t background;                  /* rt_background_type */
+    int32_t _pad;
+    double sky_intensity;                /* World.skyIntensity */
+    double solid_color[3];               /* RT_BG_SOLID color (updateBackground uses 0.1,0.1,0.1) */
+    int32_t perm[512];                   /* World.cloudNoise.p (noise.js:6-18) */
+} rt_scene_desc;
+
+typedef struct rt_settings {
+    int32_t width, height;     /* full image; pixel key p = (H-1-j)*W + i (ray-tracer.js:215) */
+    int32_t samples;           /* sampleCount of ray-tracer.js:201, resolved by the host:
+                                  1 for antiAliasing 'none', else this.samples */
+    int32_t max_depth;         /* this.maxBounces */
+    int32_t aa_mode;           /* rt_aa_mode */
+    int32_t tone_map;          /* rt_tone_map */
+    double exposure;
+    double gamma;
+    uint32_t seed;             /* keyed RNG seed */
+    int32_t sample_begin;      /* render samples [sample_begin, sample_end) of every pixel   */
+    int32_t sample_end;        /* <= 0 means sampleCount                                       */
+    int32_t crop_x0, crop_y0;  /* output window (top-down rows), crop_w/h == 0 -> full image   */
+    int32_t crop_w, crop_h;
+    int32_t precision;         /* rt_precision */
+    int32_t batch_samples;     /* samples per launch (progress/cancel granularity); 0 = all   */
+    int32_t _pad;
+} rt_settings;
+
+/* Host outputs of rt_render, each optional (NULL = not wanted). n = crop_w*crop_h pixels,
+ * top-down row-major like imageData. */
+typedef struct rt_output {
+    double* mean;          /* n*3: per-pixel linear mean, the toneMap() input (ray-tracer.js:208) */
+    float* post;           /* n*4: post-gamma floats + alpha 1.0 (the floatData of ray-tracer.js:216-219) */
+    uint8_t* rgba8;        /* n*4: min(255,max(0,floor(c*255))), NaN -> 0, alpha 255 (ray-tracer.js:226-252) */
+    uint32_t* segments;    /* n: world.hit calls per pixel (diagnostic; enables device counting) */
+    uint32_t* draws;       /* n: RNG draws per pixel (diagnostic) */
+} rt_output;
+
+typedef struct rt_stats {
+    double kernel_ms;            /* device time of the path-tracing launches (HIP events) */
+    double finalize_ms;          /* device time of the epilogue */
+    double wall_ms;              /* host wall time of the call */
+    uint64_t samples;            /* pixels x samples traced */
+    uint64_t segments;           /* world.hit calls (ray segments) */
+    uint64_t prim_tests;         /* segments x primitives tested (brute force) */
+    double algorithmic_bytes;    /* prim_tests x record bytes (+ framebuffer) */
+} rt_stats;
+
+typedef struct rt_scene rt_scene;   /* opaque: scene resident in HBM of one device */
+
+/* Library / device info. */
+int rt_abi_version(void);
+const char* rt_last_error(void);
+int rt_device_count(int* count);
+
+/* Scene lifetime: copies the descriptor into device memory of `device` (HIP ordinal). */
+int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out);
+void rt_scene_destroy(rt_scene* scene);
+
+/* Full render into host buffers: trace, finalize (tone map, gamma, RGBA8) and copy back.
+ * Replaces RayTracer.render (ray-tracer.js:166-281) minus the DOM. Synchronous.
+ * progress(fraction, user) is called between sample batches from the calling thread; a non-zero
+ * return value cancels (like window.renderCancelled, ray-tracer.js:190,196). */
+typedef int (*rt_progress_fn)(double fraction, void* user);
+int rt_render(rt_scene* scene, const rt_settings* settings, const rt_output* out,
+              rt_progress_fn progress, void* user, rt_stats* stats);
+
+/* Device-level building blocks for multi-GPU (one process per GPU): trace samples
+ * [sample_begin, sample_end) and ADD per-pixel radiance sums into d_sum (device, n*3 doubles,
+ * caller zeroes it); segment counting goes to stats.  Asynchronous on `hip_stream`
+ * (a hipStream_t, NULL = default stream); stats are filled after the stream is synchronized
+ * when `sync` is non-zero. */
+int rt_trace_device(rt_scene* scene, const rt_settings* settings, double* d_sum, void* hip_stream,
+                    int sync, rt_stats* stats);
+
+/* Epilogue on device: mean = sum / sampleCount, toneMap, gammaCorrect, RGBA8 (ray-tracer.js:208-252).
+ * Any output pointer may be NULL. All pointers are device pointers. */
+int rt_finalize_device(const rt_settings* settings, const double* d_sum, double* d_mean, float* d_post,
+                       uint8_t* d_rgba8, void* hip_stream);
+
+/* Request cancellation of an in-flight rt_render on `scene` (polled between sample batches). */
+int rt_cancel(rt_scene* scene);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_HIP_H */

@@ -1,0 +1,64 @@
+"""Loader for the reference-generated golden fixtures (tests/golden/, made by
+oracle/ref_harness/run_reference.mjs from the real /root/reference renderer)."""
+import gzip
+import json
+import os
+
+import numpy as np
+
+from blenderraytracer_amd import capi
+from blenderraytracer_amd.renderer import GpuRayTracer
+from blenderraytracer_amd.scene import load_scene_json
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+_manifest = None
+
+
+def manifest():
+    global _manifest
+    if _manifest is None:
+        with open(os.path.join(GOLDEN, "manifest.json")) as f:
+            _manifest = json.load(f)
+    return _manifest
+
+
+def case_names():
+    return sorted(manifest()["cases"].keys())
+
+
+def load_array(case, key):
+    c = manifest()["cases"][case]
+    dt = {"linear": np.float64, "post": np.float64, "rgba8": np.uint8, "segs": np.uint32, "draws": np.uint32}[key]
+    raw = gzip.open(os.path.join(GOLDEN, c["files"][key])).read()
+    _, _, cw, ch = c["crop"]
+    comp = {"linear": 3, "post": 3, "rgba8": 4, "segs": 1, "draws": 1}[key]
+    a = np.frombuffer(raw, dtype=dt).reshape(ch, cw, comp)
+    return a[..., 0] if comp == 1 else a
+
+
+def kats():
+    with gzip.open(os.path.join(GOLDEN, "kats.json.gz")) as f:
+        return decode(json.load(f))
+
+
+def decode(v):
+    if isinstance(v, str) and v in ("NaN", "Infinity", "-Infinity"):
+        return float(v.replace("Infinity", "inf"))
+    if isinstance(v, list):
+        return [decode(x) for x in v]
+    if isinstance(v, dict):
+        return {k: decode(x) for k, x in v.items()}
+    return v
+
+
+def tracer_for(case, precision=capi.RT_PREC_F64, device=0):
+    """GpuRayTracer configured exactly as the harness configured the reference RayTracer."""
+    c = manifest()["cases"][case]
+    w, h = c["requested"]
+    rt = GpuRayTracer(w, h, seed=c["seed"], device=device, precision=precision)
+    assert rt.load_from_json(load_scene_json(c["scene"]))
+    rt.update_render_settings(c["settings_in"])
+    if c["background_in"]:
+        rt.update_background(c["background_in"]["type"], c["background_in"]["intensity"])
+    assert (rt.width, rt.height) == (c["width"], c["height"])
+    return rt, c
