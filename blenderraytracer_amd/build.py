@@ -1,0 +1,79 @@
+"""Build librt_hip.so (HIP kernels + C ABI) for gfx950, in-tree, with plain hipcc.
+
+    python -m blenderraytracer_amd.build [--napi]
+
+Flags: -ffp-contract=off keeps every binary64 operation unfused, like JavaScript; no fast-math
+(NaN/Inf semantics are part of Box.hit and the JSON-solid background, SURVEY §7 hard part 1).
+The N-API addon (csrc/napi_addon.cpp, for the Node host) is built with --napi when Node headers exist.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+REPO = os.path.dirname(HERE)
+ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+
+SOURCES = ["pt_trace.hip", "rt_capi.cpp"]
+HIP_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
+             "-Wall", "-Wno-unused-function", "-I", os.path.join(REPO, "include")]
+
+
+def _run(cmd):
+    print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_lib(force=False):
+    os.makedirs(LIBDIR, exist_ok=True)
+    target = os.path.join(LIBDIR, "librt_hip.so")
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(REPO, "include", "rt_hip.h")]
+    if not force and not _stale(target, deps):
+        return target
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
+        _run([HIPCC, *HIP_FLAGS, "-c", os.path.join(CSRC, src), "-o", obj])
+        objs.append(obj)
+    _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", target, *objs])
+    return target
+
+
+def build_napi(force=False):
+    """Node N-API addon: plain g++ against node_api.h, links librt_hip.so by rpath."""
+    node_inc = os.environ.get("NODE_INCLUDE", "/usr/include/node")
+    if not os.path.exists(os.path.join(node_inc, "node_api.h")):
+        print("node_api.h not found: skipping the N-API addon")
+        return None
+    target = os.path.join(LIBDIR, "rt_napi.node")
+    src = os.path.join(CSRC, "napi_addon.cpp")
+    if not os.path.exists(src):
+        return None
+    if not force and not _stale(target, [src, os.path.join(REPO, "include", "rt_hip.h"), os.path.join(LIBDIR, "librt_hip.so")]):
+        return target
+    _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-I", node_inc, "-I", os.path.join(REPO, "include"),
+          src, "-o", target, "-L", LIBDIR, "-lrt_hip", "-Wl,-rpath,$ORIGIN"])
+    return target
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    force = "--force" in argv
+    print(build_lib(force))
+    if "--napi" in argv:
+        print(build_napi(force))
+
+
+if __name__ == "__main__":
+    main()

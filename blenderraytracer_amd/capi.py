@@ -94,6 +94,12 @@ def load_library(path=None):
     if _lib is not None and path is None:
         return _lib
     p = path or os.environ.get("RT_HIP_LIB", LIB_PATH)
+    try:
+        # torch ships its own libamdhip64.so (same soname): load it first so that this process has
+        # ONE HIP runtime and torch device pointers are valid inside librt_hip.so
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(p):
         raise RuntimeError(f"librt_hip.so not found at {p}: run `python -m blenderraytracer_amd.build` "
                            "(the HIP backend has no CPU fallback)")

@@ -1,0 +1,316 @@
+// pt_core.h — device-side building blocks of the path-tracing megakernel (gfx950).
+//
+// Everything is templated on the arithmetic type R:
+//   R = double : the reference's own arithmetic (JS numbers), compiled with -ffp-contract=off so
+//                every + - * / sqrt is one correctly rounded binary64 op in the JS evaluation order.
+//                Ray paths then follow the reference decision for decision (tests/test_gpu_parity.py).
+//   R = float  : fast mode; same algorithm in binary32.
+// Reference citations are js/<file>:<line> in Shinzef/BlenderRayTracer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+// Path code is __host__ __device__ so that tests/hostcheck can run the kernel's exact per-lane
+// logic on the CPU (test infrastructure only; librt_hip.so has no host execution path).
+#define RT_HD __host__ __device__ __forceinline__
+
+namespace rt {
+
+// ---- keyed RNG ------------------------------------------------------------------
+RT_HD uint32_t lowbias32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16; return x;
+}
+RT_HD uint32_t pixel_key(uint32_t seedm, uint32_t pixel) { return lowbias32(seedm ^ pixel); }
+RT_HD uint32_t sample_key(uint32_t pkey, uint32_t sample) {
+    return lowbias32(pkey ^ lowbias32(sample + 0x1B873593U));
+}
+
+template <class R>
+struct Rng {
+    uint32_t key, k;
+    RT_HD R next() {
+        uint32_t h = lowbias32(key ^ (k * 0x9E3779B9U));
+        ++k;
+        return (R)(h >> 8) * (R)(1.0 / 16777216.0);   // exact in f32 and f64
+    }
+};
+
+// ---- JS semantics helpers ----------------------------------------------------------------------
+template <class R> RT_HD R js_max(R a, R b) {   // Math.max: NaN-propagating
+    return (a != a || b != b) ? (R)NAN : (a > b ? a : b);
+}
+template <class R> RT_HD R js_min(R a, R b) {
+    return (a != a || b != b) ? (R)NAN : (a < b ? a : b);
+}
+
+template <class R> struct V3 { R x, y, z; };
+template <class R> RT_HD V3<R> mk(R x, R y, R z) { return V3<R>{x, y, z}; }
+template <class R> RT_HD V3<R> operator+(V3<R> a, V3<R> b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+template <class R> RT_HD V3<R> operator-(V3<R> a, V3<R> b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+template <class R> RT_HD V3<R> operator*(V3<R> a, R s) { return {a.x * s, a.y * s, a.z * s}; }
+template <class R> RT_HD V3<R> vdiv(V3<R> a, R s) { return {a.x / s, a.y / s, a.z / s}; }
+template <class R> RT_HD R dot(V3<R> a, V3<R> b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+template <class R> RT_HD V3<R> cross(V3<R> a, V3<R> b) {
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+template <class R> RT_HD V3<R> normalize(V3<R> a) {          // math.js:18
+    R l = sqrt(a.x * a.x + a.y * a.y + a.z * a.z);
+    return l > (R)0 ? vdiv(a, l) : mk<R>(0, 0, 0);
+}
+template <class R> RT_HD V3<R> reflect(V3<R> a, V3<R> n) {   // math.js:19
+    return a - n * ((R)2 * dot(a, n));
+}
+
+// ---- scene records in HBM (built by rt_scene_create) ---------------------------------------------
+enum RunKind : int { RUN_SPHERES = 0, RUN_PLANES = 1, RUN_BOXES = 2, RUN_TRIANGLES = 3, RUN_MESH = 4 };
+struct Run { int kind, begin, end, mat; };   // consecutive world objects of one kind (mat: mesh material)
+
+template <class R> struct SphereRec { R cx, cy, cz, r2; };            // r2 = radius*radius (geometry.js:19)
+template <class R> struct PlaneRec { R px, py, pz, nx, ny, nz; };
+template <class R> struct BoxRec { R mnx, mny, mnz, mxx, mxy, mxz; };
+template <class R> struct TriRec { R v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z, nx, ny, nz; };  // e1=v1-v0, e2=v2-v0
+template <class R> struct MatRec { int type, pad; R albedo[3]; R rough; R ior; R emit[3]; };
+
+template <class R>
+struct SceneView {
+    const Run* runs;
+    int num_runs;
+    int num_prims;                 // primitives tested per segment (brute force)
+    const SphereRec<R>* spheres;
+    const R* sphere_r;             // radius (normal = (p - c) / r, geometry.js:34)
+    const PlaneRec<R>* planes;
+    const BoxRec<R>* boxes;
+    const TriRec<R>* tris;
+    const int* sphere_mat;
+    const int* plane_mat;
+    const int* box_mat;
+    const int* tri_mat;            // per triangle (mesh triangles carry the mesh's material)
+    const MatRec<R>* mats;
+    const int* perm;               // World.cloudNoise.p[512]
+    // camera (camera.js:8-36 vectors, computed on the host in binary64)
+    R cam_o[3], cam_llc[3], cam_h[3], cam_v[3], cam_u[3], cam_vv[3], cam_w[3];
+    R lens_radius;
+    int cam_ortho;
+    int background;
+    R sky_intensity;
+    R solid[3];
+};
+
+enum HitKind : int { HIT_NONE = -1, HIT_SPHERE = 0, HIT_PLANE = 1, HIT_BOX = 2, HIT_TRI = 3 };
+
+template <class R>
+struct Closest { R t; int kind, idx, mat; };
+
+// Closest hit over the whole world: World.hit (world.js:20-33) with every object's hit() inlined.
+// All lanes walk the same primitive list in the same order, so every record load — including the
+// material index, taken at accept time — is wave-uniform (scalar loads, no LDS).  Only
+// (t, kind, index, material) is tracked; the hit record is rebuilt afterwards from (t, primitive),
+// which is exact because no primitive's chosen t depends on tMax.
+template <class R>
+RT_HD Closest<R> closest_hit(const SceneView<R>& sc, V3<R> o, V3<R> d) {
+    const R tmin = (R)0.001;
+    Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0};
+    const R a = dot(d, d);
+    for (int r = 0; r < sc.num_runs; ++r) {
+        const Run run = sc.runs[r];
+        if (run.kind == RUN_SPHERES) {
+#pragma unroll 2
+            for (int i = run.begin; i < run.end; ++i) {                       // geometry.js:15-45
+                const SphereRec<R> s = sc.spheres[i];
+                R ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
+                R hb = ocx * d.x + ocy * d.y + ocz * d.z;
+                R c = (ocx * ocx + ocy * ocy + ocz * ocz) - s.r2;
+                R disc = hb * hb - a * c;
+                if (!(disc < (R)0)) {
+                    R sq = sqrt(disc);
+                    R root = (-hb - sq) / a;
+                    bool ok = true;
+                    if (root < tmin || b.t < root) {
+                        root = (-hb + sq) / a;
+                        ok = !(root < tmin || b.t < root);
+                    }
+                    if (ok && root < b.t) b = Closest<R>{root, HIT_SPHERE, i, sc.sphere_mat[i]};
+                }
+            }
+        } else if (run.kind == RUN_PLANES) {
+            for (int i = run.begin; i < run.end; ++i) {                       // geometry.js:56-74
+                const PlaneRec<R> p = sc.planes[i];
+                R denom = p.nx * d.x + p.ny * d.y + p.nz * d.z;
+                if (fabs(denom) < (R)1e-6) continue;
+                R t = ((p.px - o.x) * p.nx + (p.py - o.y) * p.ny + (p.pz - o.z) * p.nz) / denom;
+                if (t < tmin || t > b.t) continue;
+                if (t < b.t) b = Closest<R>{t, HIT_PLANE, i, sc.plane_mat[i]};
+            }
+        } else if (run.kind == RUN_BOXES) {
+            for (int i = run.begin; i < run.end; ++i) {                       // geometry.js:85-117
+                const BoxRec<R> bx = sc.boxes[i];
+                R t0 = (bx.mnx - o.x) / d.x, t1 = (bx.mxx - o.x) / d.x;
+                if (t0 > t1) { R s = t0; t0 = t1; t1 = s; }
+                R ty0 = (bx.mny - o.y) / d.y, ty1 = (bx.mxy - o.y) / d.y;
+                if (ty0 > ty1) { R s = ty0; ty0 = ty1; ty1 = s; }
+                if (t0 > ty1 || ty0 > t1) continue;
+                t0 = js_max(t0, ty0);
+                t1 = js_min(t1, ty1);
+                R tz0 = (bx.mnz - o.z) / d.z, tz1 = (bx.mxz - o.z) / d.z;
+                if (tz0 > tz1) { R s = tz0; tz0 = tz1; tz1 = s; }
+                if (t0 > tz1 || tz0 > t1) continue;
+                t0 = js_max(t0, tz0);
+                t1 = js_min(t1, tz1);
+                R t = t0 > tmin ? t0 : t1;
+                if (t < tmin || t > b.t) continue;                            // NaN passes here ...
+                if (t < b.t) b = Closest<R>{t, HIT_BOX, i, sc.box_mat[i]};    // ... and fails here
+            }
+        } else {                                                              // geometry.js:148-188, 248-262
+            const bool mesh = run.kind == RUN_MESH;
+            R local = b.t;
+            int local_idx = -1;
+            for (int i = run.begin; i < run.end; ++i) {
+                const TriRec<R> tr = sc.tris[i];
+                // h = d x e2 ; a = e1 . h
+                R hx = d.y * tr.e2z - d.z * tr.e2y, hy = d.z * tr.e2x - d.x * tr.e2z, hz = d.x * tr.e2y - d.y * tr.e2x;
+                R aa = tr.e1x * hx + tr.e1y * hy + tr.e1z * hz;
+                if (fabs(aa) < (R)0.0001) continue;
+                R f = (R)1 / aa;
+                R sx = o.x - tr.v0x, sy = o.y - tr.v0y, sz = o.z - tr.v0z;
+                R u = f * (sx * hx + sy * hy + sz * hz);
+                if (u < (R)0 || u > (R)1) continue;
+                R qx = sy * tr.e1z - sz * tr.e1y, qy = sz * tr.e1x - sx * tr.e1z, qz = sx * tr.e1y - sy * tr.e1x;
+                R v = f * (d.x * qx + d.y * qy + d.z * qz);
+                if (v < (R)0 || u + v > (R)1) continue;
+                R t = f * (tr.e2x * qx + tr.e2y * qy + tr.e2z * qz);
+                if (t < tmin || t > local) continue;
+                if (mesh) { local = t; local_idx = i; }                       // mesh: <=, last equal-t wins
+                else if (t < b.t) { local = t; b = Closest<R>{t, HIT_TRI, i, sc.tri_mat[i]}; }
+            }
+            if (mesh && local_idx >= 0 && local < b.t) b = Closest<R>{local, HIT_TRI, local_idx, run.mat};
+        }
+    }
+    return b;
+}
+
+template <class R>
+struct Hit { V3<R> p, n; bool front; int mat; };
+
+template <class R>
+RT_HD void set_face(Hit<R>& h, V3<R> d, V3<R> outward) {       // math.js:55-58
+    h.front = dot(d, outward) < (R)0;
+    h.n = h.front ? outward : outward * (R)-1;
+}
+
+// Rebuild the HitRecord of the winning primitive (point = origin + dir*t, math.js:41).
+template <class R>
+RT_HD Hit<R> hit_record(const SceneView<R>& sc, V3<R> o, V3<R> d, const Closest<R>& c) {
+    Hit<R> h;
+    h.p = o + d * c.t;
+    h.mat = c.mat;
+    if (c.kind == HIT_SPHERE) {
+        const SphereRec<R> s = sc.spheres[c.idx];
+        set_face(h, d, vdiv(h.p - mk(s.cx, s.cy, s.cz), sc.sphere_r[c.idx]));
+    } else if (c.kind == HIT_PLANE) {
+        const PlaneRec<R> p = sc.planes[c.idx];
+        set_face(h, d, mk(p.nx, p.ny, p.nz));
+    } else if (c.kind == HIT_BOX) {                                                   // geometry.js:118-126
+        const BoxRec<R> b = sc.boxes[c.idx];
+        const R eps = (R)1e-6;
+        V3<R> n;
+        if (fabs(h.p.x - b.mnx) < eps) n = mk<R>(-1, 0, 0);
+        else if (fabs(h.p.x - b.mxx) < eps) n = mk<R>(1, 0, 0);
+        else if (fabs(h.p.y - b.mny) < eps) n = mk<R>(0, -1, 0);
+        else if (fabs(h.p.y - b.mxy) < eps) n = mk<R>(0, 1, 0);
+        else if (fabs(h.p.z - b.mnz) < eps) n = mk<R>(0, 0, -1);
+        else n = mk<R>(0, 0, 1);
+        set_face(h, d, n);
+    } else {
+        const TriRec<R> tr = sc.tris[c.idx];
+        set_face(h, d, mk(tr.nx, tr.ny, tr.nz));
+    }
+    return h;
+}
+
+template <class R>
+RT_HD V3<R> random_in_unit_sphere(Rng<R>& g) {                  // math.js:22-26
+    V3<R> p;
+    do {
+        R a = g.next(), b = g.next(), c = g.next();
+        p = mk(a * (R)2 - (R)1, b * (R)2 - (R)1, c * (R)2 - (R)1);
+    } while (dot(p, p) >= (R)1);
+    return p;
+}
+
+template <class R>
+RT_HD V3<R> random_in_unit_disk(Rng<R>& g) {                    // math.js:27-31
+    R x, y;
+    do {
+        x = g.next() * (R)2 - (R)1;
+        y = g.next() * (R)2 - (R)1;
+    } while (x * x + y * y + (R)0 * (R)0 >= (R)1);
+    return mk<R>(x, y, 0);
+}
+
+// ---- backgrounds (world.js:35-110, Perlin noise.js:29-61) ---------------------------------------
+template <class R> RT_HD R fade(R t) { return t * t * t * (t * (t * (R)6 - (R)15) + (R)10); }
+template <class R> RT_HD R lerp(R t, R a, R b) { return a + t * (b - a); }
+template <class R> RT_HD R grad(int hash, R x, R y, R z) {
+    int h = hash & 15;
+    R u = h < 8 ? x : y;
+    R v = h < 4 ? y : (h == 12 || h == 14) ? x : z;
+    return ((h & 1) == 0 ? u : -u) + ((h & 2) == 0 ? v : -v);
+}
+template <class R>
+__host__ __device__ R perlin(const int* p, R x, R y, R z) {
+    R fx0 = floor(x), fy0 = floor(y), fz0 = floor(z);
+    int X = ((int)(long long)fx0) & 255, Y = ((int)(long long)fy0) & 255, Z = ((int)(long long)fz0) & 255;
+    R fx = x - fx0, fy = y - fy0, fz = z - fz0;
+    R u = fade(fx), v = fade(fy), w = fade(fz);
+    int A = p[X] + Y, AA = p[A] + Z, AB = p[A + 1] + Z;
+    int B = p[X + 1] + Y, BA = p[B] + Z, BB = p[B + 1] + Z;
+    return lerp(w,
+                lerp(v, lerp(u, grad(p[AA], fx, fy, fz), grad(p[BA], fx - (R)1, fy, fz)),
+                     lerp(u, grad(p[AB], fx, fy - (R)1, fz), grad(p[BB], fx - (R)1, fy - (R)1, fz))),
+                lerp(v, lerp(u, grad(p[AA + 1], fx, fy, fz - (R)1), grad(p[BA + 1], fx - (R)1, fy, fz - (R)1)),
+                     lerp(u, grad(p[AB + 1], fx, fy - (R)1, fz - (R)1), grad(p[BB + 1], fx - (R)1, fy - (R)1, fz - (R)1))));
+}
+
+template <class R>
+__host__ __device__ V3<R> background(const SceneView<R>& sc, V3<R> d) {
+    const R I = sc.sky_intensity;
+    switch (sc.background) {
+    case 0: {                                                                         // skyGradient
+        R t = (R)0.5 * (normalize(d).y + (R)1);
+        return (mk<R>(1, 1, 1) * ((R)1 - t) + mk<R>(0.5, 0.7, 1.0) * t) * I;
+    }
+    case 1:                                                                           // solid
+        return mk(sc.solid[0], sc.solid[1], sc.solid[2]) * I;
+    case 2: {                                                                         // hdri
+        V3<R> dir = normalize(d);
+        V3<R> sun = normalize(mk<R>(-0.3, 0.6, -0.5));
+        R sd = js_max<R>(0, dot(dir, sun));
+        R mask = sd > ((R)1 - (R)0.04) ? (R)1 : (R)0;
+        V3<R> sun_c = mk<R>(1.0, 0.95, 0.8) * (mask * (R)20);
+        R corona = js_max<R>(0, (sd - ((R)1 - (R)0.2)) / (R)0.2);
+        V3<R> cor_c = mk<R>(1.0, 0.8, 0.6) * (pow(corona, (R)2) * (R)3);
+        R y = dir.y;
+        V3<R> sky_c = mk<R>(0.3, 0.5, 0.8) * (js_max<R>(0, y * (R)0.5 + (R)0.5) * (R)2);
+        V3<R> gnd_c = mk<R>(0.2, 0.15, 0.1) * js_max<R>(0, -y * (R)0.3);
+        V3<R> sc_c = mk<R>(0.8, 0.9, 1.0) * (pow(js_max<R>(0, (R)1 - fabs(y)), (R)2) * (R)0.3);
+        return ((((sky_c + gnd_c) + sc_c) + sun_c) + cor_c) * I;
+    }
+    case 3: {                                                                         // proceduralSky
+        V3<R> dir = normalize(d);
+        V3<R> sun = normalize(mk<R>(0.3, 0.6, 0.8));
+        R sd = js_max<R>(0, dot(dir, sun));
+        V3<R> sun_c = mk<R>(1.0, 0.95, 0.8) * (pow(sd, (R)512) * (R)10);
+        V3<R> sky_c = mk<R>(0.4, 0.7, 1.0) * (js_max<R>(0, dir.y) * (R)0.8);
+        V3<R> glow_c = mk<R>(1.0, 0.8, 0.6) * (exp(-fabs(dir.y) * (R)4) * (R)0.3);
+        V3<R> gnd_c = mk<R>(0.1, 0.15, 0.1) * js_max<R>(0, -dir.y * (R)0.5);
+        R cloud = js_max<R>(0, perlin<R>(sc.perm, dir.x * (R)10, dir.y * (R)3 + (R)2, dir.z * (R)10) * (R)0.8 + (R)0.2);
+        V3<R> cl_c = mk<R>(0.9, 0.9, 1.0) * (cloud * js_max<R>(0, dir.y) * (R)0.5);
+        return ((((sky_c + glow_c) + gnd_c) + sun_c) + cl_c) * I;
+    }
+    default:                                                                          // JSON solid/hdri bug
+        return mk<R>((R)NAN, (R)NAN, (R)NAN);
+    }
+}
+
+}  // namespace rt

@@ -1,0 +1,29 @@
+// pt_launch.h — host-visible launch interface of the path-tracing kernels (pt_trace.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pt_path.h"
+
+namespace rt {
+
+struct Counters {
+    double* sum;               // n*3 running per-pixel radiance sums (read-modify-write)
+    uint32_t* segs;            // optional n per-pixel world.hit counts
+    uint32_t* draws;           // optional n per-pixel RNG draws
+    unsigned long long* total_segs;   // optional global segment counter
+};
+
+template <class R>
+hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, hipStream_t stream);
+
+struct FinalizeParams {
+    int n;
+    int samples;
+    int tone_map;
+    double exposure, gamma;
+};
+hipError_t launch_finalize(const FinalizeParams& p, const double* sum, double* mean, float* post, uint8_t* rgba8,
+                           hipStream_t stream);
+
+}  // namespace rt

@@ -1,0 +1,147 @@
+// pt_path.h — the per-lane body of the megakernel: one pixel, samples [s_begin, s_end).
+//
+// The recursion of rayColor (js/ray-tracer.js:102-123) is flattened into one loop whose body is
+// exactly one world.hit: when a path terminates (miss, emissive, absorption, depth cap) the lane
+// adds its radiance to the pixel sum and immediately regenerates the camera ray of its next sample
+// (path regeneration), so the lanes of a wave stay busy until their pixel is done.
+// Radiance is carried as a forward throughput product T (att_0*att_1*...)*E instead of the
+// recursion's att_0*(att_1*(...*E)): the same factors, rounded in a different order (<= a few ulp);
+// every path DECISION is unaffected.
+#pragma once
+#include "pt_core.h"
+
+namespace rt {
+
+struct ImageParams {
+    int width, height;         // full image (pixel keys)
+    int x0, y0, cw, ch;        // crop window (top-down rows)
+    int samples;               // sampleCount (divisor of the mean)
+    int s_begin, s_end;        // sample range of this launch
+    int max_depth;
+    int aa_mode;
+    uint32_t seedm;            // seed_mix(seed)
+};
+
+template <class R>
+RT_HD void start_sample(const SceneView<R>& sc, const ImageParams& im, int i, int j, uint32_t pkey, int s, Rng<R>& g,
+                        V3<R>& o, V3<R>& d) {
+    g.key = sample_key(pkey, (uint32_t)s);
+    g.k = 0;
+    R u, v;                                                                   // ray-tracer.js:125-149
+    if (im.aa_mode == 1) {
+        R r1 = g.next(), r2 = g.next();
+        R ox = sqrt(r1) * cos((R)2 * (R)3.141592653589793 * r2);
+        R oy = sqrt(r1) * sin((R)2 * (R)3.141592653589793 * r2);
+        u = ((R)i + (R)0.5 + ox * (R)0.5) / (R)im.width;
+        v = ((R)j + (R)0.5 + oy * (R)0.5) / (R)im.height;
+    } else if (im.aa_mode == 0) {
+        u = ((R)i + g.next()) / (R)im.width;
+        v = ((R)j + g.next()) / (R)im.height;
+    } else {
+        u = ((R)i + (R)0.5) / (R)im.width;
+        v = ((R)j + (R)0.5) / (R)im.height;
+    }
+    const V3<R> cu = mk(sc.cam_u[0], sc.cam_u[1], sc.cam_u[2]);               // camera.js:38-51
+    const V3<R> cv = mk(sc.cam_vv[0], sc.cam_vv[1], sc.cam_vv[2]);
+    const V3<R> co = mk(sc.cam_o[0], sc.cam_o[1], sc.cam_o[2]);
+    const V3<R> llc = mk(sc.cam_llc[0], sc.cam_llc[1], sc.cam_llc[2]);
+    const V3<R> hor = mk(sc.cam_h[0], sc.cam_h[1], sc.cam_h[2]);
+    const V3<R> ver = mk(sc.cam_v[0], sc.cam_v[1], sc.cam_v[2]);
+    V3<R> rd = random_in_unit_disk(g) * sc.lens_radius;
+    if (sc.cam_ortho) {
+        o = (co + cu * rd.x) + cv * rd.y;
+        d = normalize((((llc + hor * u) + ver * v) - o) + mk(sc.cam_w[0], sc.cam_w[1], sc.cam_w[2]) * (R)-1);
+    } else {
+        o = co + (cu * rd.x + cv * rd.y);
+        d = ((llc + hor * u) + ver * v) - o;
+    }
+}
+
+// Scatter at a non-emissive hit (materials.js:20-83).  Returns false when Metal absorbs.
+template <class R>
+RT_HD bool scatter(const MatRec<R>& m, const Hit<R>& h, V3<R> d, Rng<R>& g, V3<R>& nd, V3<R>& att) {
+    if (m.type == 0) {                                                        // Lambertian :20-25
+        nd = h.n + normalize(random_in_unit_sphere(g));
+        att = mk(m.albedo[0], m.albedo[1], m.albedo[2]);
+        return true;
+    }
+    if (m.type == 1) {                                                        // Metal :36-41
+        V3<R> refl = reflect(normalize(d), h.n);
+        nd = refl + random_in_unit_sphere(g) * m.rough;
+        att = mk(m.albedo[0], m.albedo[1], m.albedo[2]);
+        return dot(nd, h.n) > (R)0;
+    }
+    R ratio = h.front ? ((R)1 / m.ior) : m.ior;                               // Dielectric :51-83
+    V3<R> unit = normalize(d);
+    R cos_t = js_min<R>(dot(unit * (R)-1, h.n), (R)1);
+    R sin_t = sqrt((R)1 - cos_t * cos_t);
+    bool reflect_it = ratio * sin_t > (R)1;
+    if (!reflect_it) {                                                        // random drawn only if it can refract
+        R r0 = ((R)1 - ratio) / ((R)1 + ratio);
+        r0 = r0 * r0;
+        R refl = r0 + ((R)1 - r0) * pow((R)1 - cos_t, (R)5);
+        reflect_it = refl > g.next();
+    }
+    if (reflect_it) {
+        nd = reflect(unit, h.n);
+    } else {
+        R ct = js_min<R>(dot(unit * (R)-1, h.n), (R)1);
+        V3<R> perp = (unit + h.n * ct) * ratio;
+        V3<R> par = h.n * (-sqrt(fabs((R)1 - dot(perp, perp))));
+        nd = perp + par;
+    }
+    att = mk<R>(1, 1, 1);
+    return true;
+}
+
+struct PixelResult { uint32_t segments, draws; };
+
+// Trace samples [im.s_begin, s_end) of crop pixel (cx, cy), adding radiance into sum[0..2].
+template <class R, bool COUNT>
+RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int cx, int cy, int s_end, double* sum) {
+    const int i = im.x0 + cx, row = im.y0 + cy, j = im.height - 1 - row;
+    const uint32_t pkey = pixel_key(im.seedm, (uint32_t)row * (uint32_t)im.width + (uint32_t)i);
+    PixelResult res{0, 0};
+    int s = im.s_begin;
+    double sx = sum[0], sy = sum[1], sz = sum[2];
+    Rng<R> g;
+    V3<R> o, d, T = mk<R>(1, 1, 1);
+    int depth = im.max_depth;
+    if (s < s_end) start_sample(sc, im, i, j, pkey, s, g, o, d);
+    while (s < s_end) {
+        const Closest<R> c = closest_hit(sc, o, d);
+        ++res.segments;
+        bool done = true;
+        V3<R> L = mk<R>(0, 0, 0);
+        if (c.kind != HIT_NONE) {
+            const Hit<R> h = hit_record(sc, o, d, c);
+            const MatRec<R> m = sc.mats[h.mat];
+            if (m.type == 3) {                                                // Emissive (materials.js:87-96)
+                L = mk(T.x * m.emit[0], T.y * m.emit[1], T.z * m.emit[2]);
+            } else {
+                V3<R> nd, att;
+                if (scatter(m, h, d, g, nd, att)) {
+                    T = mk(T.x * att.x, T.y * att.y, T.z * att.z);
+                    o = h.p;
+                    d = nd;
+                    done = --depth <= 0;                                      // rayColor(.., 0) returns 0
+                }
+            }
+        } else {
+            V3<R> bg = background(sc, d);                                     // world.background(ray)
+            L = mk(T.x * bg.x, T.y * bg.y, T.z * bg.z);
+        }
+        if (done) {
+            sx += (double)L.x; sy += (double)L.y; sz += (double)L.z;
+            if (COUNT) res.draws += g.k;
+            ++s;
+            T = mk<R>(1, 1, 1);
+            depth = im.max_depth;
+            if (s < s_end) start_sample(sc, im, i, j, pkey, s, g, o, d);
+        }
+    }
+    sum[0] = sx; sum[1] = sy; sum[2] = sz;
+    return res;
+}
+
+}  // namespace rt

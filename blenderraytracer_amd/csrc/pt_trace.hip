@@ -1,0 +1,98 @@
+// pt_trace.hip — the path-tracing megakernel and its epilogue for gfx950 (MI355X).
+//
+// One lane owns one pixel of the crop window and traces that pixel's samples [s_begin, s_end) in
+// order (trace_pixel, pt_path.h).  A 256-thread workgroup covers a 16x16 tile, each wave an 8x8
+// block, so neighbouring rays share a wave.  Primitive records are walked in World.objects order by
+// every lane in lockstep, so all record loads are wave-uniform scalar loads; the per-pixel sums are
+// read and written once per launch.
+#include "pt_launch.h"
+
+namespace rt {
+
+template <class R>
+struct TraceArgs {
+    SceneView<R> sc;
+    ImageParams im;
+    Counters c;
+};
+
+template <class R, bool COUNT>
+__global__ __launch_bounds__(256) void trace_kernel(const TraceArgs<R> args) {
+    const ImageParams& im = args.im;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int tiles_x = (im.cw + 15) >> 4;
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int cx = tx * 16 + (wave & 1) * 8 + (lane & 7);                    // 8x8 pixels per wave
+    const int cy = ty * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const bool valid = cx < im.cw && cy < im.ch;
+    const size_t q = (size_t)cy * im.cw + cx;
+    double acc[3] = {0, 0, 0};
+    if (valid) { acc[0] = args.c.sum[3 * q]; acc[1] = args.c.sum[3 * q + 1]; acc[2] = args.c.sum[3 * q + 2]; }
+    // invalid lanes trace nothing but stay for the wave reduction below
+    const PixelResult r = trace_pixel<R, COUNT>(args.sc, im, cx, cy, valid ? im.s_end : im.s_begin, acc);
+    if (valid) {
+        args.c.sum[3 * q] = acc[0]; args.c.sum[3 * q + 1] = acc[1]; args.c.sum[3 * q + 2] = acc[2];
+        if (COUNT) {
+            if (args.c.segs) args.c.segs[q] += r.segments;
+            if (args.c.draws) args.c.draws[q] += r.draws;
+        }
+    }
+    if (args.c.total_segs) {
+        unsigned long long v = r.segments;
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) atomicAdd(args.c.total_segs, v);
+    }
+}
+
+template <class R>
+hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, hipStream_t stream) {
+    if (im.cw <= 0 || im.ch <= 0 || im.s_end <= im.s_begin) return hipSuccess;
+    const int tiles = ((im.cw + 15) >> 4) * ((im.ch + 15) >> 4);
+    TraceArgs<R> a{sc, im, c};
+    if (c.segs || c.draws)
+        hipLaunchKernelGGL((trace_kernel<R, true>), dim3(tiles), dim3(256), 0, stream, a);
+    else
+        hipLaunchKernelGGL((trace_kernel<R, false>), dim3(tiles), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+template hipError_t launch_trace<double>(const SceneView<double>&, const ImageParams&, const Counters&, hipStream_t);
+template hipError_t launch_trace<float>(const SceneView<float>&, const ImageParams&, const Counters&, hipStream_t);
+
+// ---- epilogue: mean, toneMap, gammaCorrect, RGBA8 (ray-tracer.js:208-252, post-processor.js:9-42) ----
+__device__ __forceinline__ uint8_t to_u8(double c) {
+    double v = js_min<double>(255.0, js_max<double>(0.0, floor(c * 255.0)));
+    return v != v ? (uint8_t)0 : (uint8_t)v;                  // Uint8ClampedArray stores NaN as 0
+}
+
+__global__ __launch_bounds__(256) void finalize_kernel(const FinalizeParams p, const double* __restrict__ sum,
+                                                       double* __restrict__ mean, float* __restrict__ post,
+                                                       uint8_t* __restrict__ rgba8) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= p.n) return;
+    double c[3], g[3];
+    const double inv_gamma = 1.0 / p.gamma;
+    for (int k = 0; k < 3; ++k) c[k] = sum[3 * q + k] / (double)p.samples;
+    if (mean) { mean[3 * q] = c[0]; mean[3 * q + 1] = c[1]; mean[3 * q + 2] = c[2]; }
+    for (int k = 0; k < 3; ++k) {
+        double x = c[k] * p.exposure, tm;
+        if (p.tone_map == 1) tm = js_max<double>(0.0, (x * (2.51 * x + 0.03)) / (x * (2.43 * x + 0.59) + 0.14));
+        else if (p.tone_map == 2) tm = x;
+        else tm = x / (1.0 + x);
+        g[k] = pow(js_max<double>(0.0, tm), inv_gamma);
+    }
+    if (post) *reinterpret_cast<float4*>(post + 4 * q) = make_float4((float)g[0], (float)g[1], (float)g[2], 1.0f);
+    if (rgba8) {
+        uchar4 o = make_uchar4(to_u8(g[0]), to_u8(g[1]), to_u8(g[2]), 255);
+        *reinterpret_cast<uchar4*>(rgba8 + 4 * q) = o;
+    }
+}
+
+hipError_t launch_finalize(const FinalizeParams& p, const double* sum, double* mean, float* post, uint8_t* rgba8,
+                           hipStream_t stream) {
+    if (p.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(finalize_kernel, dim3((p.n + 255) / 256), dim3(256), 0, stream, p, sum, mean, post, rgba8);
+    return hipGetLastError();
+}
+
+}  // namespace rt

@@ -1,0 +1,373 @@
+// rt_capi.cpp — extern "C" ABI of librt_hip.so (include/rt_hip.h).
+//
+// Replaces RayTracer.render (js/ray-tracer.js:166-281): the host hands over the packed World /
+// Camera once (rt_scene_create uploads it to HBM), then each render traces sample batches on the
+// GPU, runs the epilogue on the GPU and copies back only the per-pixel outputs.
+// There is no CPU fallback anywhere in this library: without a HIP device every call fails with
+// RT_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_hip.h"
+#include "pt_launch.h"
+#include "scene_pack.h"
+
+using namespace rt;
+
+namespace {
+
+thread_local std::string g_error;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) return fail(RT_ERR_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t count) {
+        if (count <= n && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(count, 1) * sizeof(T));
+        if (e == hipSuccess) n = std::max<size_t>(count, 1);
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+template <class T>
+hipError_t upload(DevBuf<T>& b, const std::vector<T>& v) {
+    hipError_t e = b.ensure(v.size());
+    if (e != hipSuccess) return e;
+    if (!v.empty()) e = hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+    return e;
+}
+
+// Scene arrays of one precision, resident in HBM.
+template <class R>
+struct DeviceScene {
+    DevBuf<Run> runs;
+    DevBuf<SphereRec<R>> spheres;
+    DevBuf<R> sphere_r;
+    DevBuf<PlaneRec<R>> planes;
+    DevBuf<BoxRec<R>> boxes;
+    DevBuf<TriRec<R>> tris;
+    DevBuf<int> sphere_mat, plane_mat, box_mat, tri_mat, perm;
+    DevBuf<MatRec<R>> mats;
+    SceneView<R> view{};
+    void release() {
+        runs.release(); spheres.release(); sphere_r.release(); planes.release(); boxes.release(); tris.release();
+        sphere_mat.release(); plane_mat.release(); box_mat.release(); tri_mat.release(); perm.release(); mats.release();
+    }
+};
+
+template <class R>
+int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d) {
+    HostRecords<R> rec;
+    make_records(hs, d, rec);
+    hipError_t e = hipSuccess;
+#define UP(buf, vec) if (e == hipSuccess) e = upload(ds.buf, vec)
+    UP(runs, hs.runs); UP(spheres, rec.spheres); UP(sphere_r, rec.sphere_r); UP(planes, rec.planes);
+    UP(boxes, rec.boxes); UP(tris, rec.tris); UP(sphere_mat, hs.sphere_mat); UP(plane_mat, hs.plane_mat);
+    UP(box_mat, hs.box_mat); UP(tri_mat, hs.tri_mat); UP(perm, rec.perm); UP(mats, rec.mats);
+#undef UP
+    if (e != hipSuccess) return fail(RT_ERR_DEVICE, "scene upload: %s", hipGetErrorString(e));
+    SceneView<R>& v = ds.view;
+    v.runs = ds.runs.p;
+    v.spheres = ds.spheres.p; v.sphere_r = ds.sphere_r.p; v.planes = ds.planes.p; v.boxes = ds.boxes.p;
+    v.tris = ds.tris.p; v.sphere_mat = ds.sphere_mat.p; v.plane_mat = ds.plane_mat.p; v.box_mat = ds.box_mat.p;
+    v.tri_mat = ds.tri_mat.p; v.mats = ds.mats.p; v.perm = ds.perm.p;
+    fill_view_constants(v, hs, d);
+    return RT_OK;
+}
+
+double now_ms() {
+    using namespace std::chrono;
+    return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+struct rt_scene {
+    int device = 0;
+    DeviceScene<double> s64;
+    DeviceScene<float> s32;
+    int num_prims = 0;
+    double record_bytes = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {};
+    DevBuf<double> sum, mean;
+    DevBuf<float> post;
+    DevBuf<uint8_t> rgba;
+    DevBuf<uint32_t> segs, draws;
+    DevBuf<unsigned long long> total;
+    std::atomic<int> cancel{0};
+};
+
+namespace {
+
+int check_settings(const rt_settings* s, int* cw, int* ch) {
+    if (!s) return fail(RT_ERR_INVALID, "settings is NULL");
+    if (s->width <= 0 || s->height <= 0) return fail(RT_ERR_INVALID, "image %dx%d", s->width, s->height);
+    if ((long long)s->width * s->height > 0xFFFFFFFFLL) return fail(RT_ERR_INVALID, "image too large for 32-bit pixel keys");
+    *cw = s->crop_w > 0 ? s->crop_w : s->width;
+    *ch = s->crop_h > 0 ? s->crop_h : s->height;
+    if (s->crop_x0 < 0 || s->crop_y0 < 0 || s->crop_x0 + *cw > s->width || s->crop_y0 + *ch > s->height)
+        return fail(RT_ERR_INVALID, "crop [%d,%d %dx%d] outside %dx%d", s->crop_x0, s->crop_y0, *cw, *ch, s->width,
+                    s->height);
+    if (s->samples < 0) return fail(RT_ERR_INVALID, "samples %d", s->samples);
+    if (s->precision != RT_PREC_F64 && s->precision != RT_PREC_F32) return fail(RT_ERR_INVALID, "precision %d", s->precision);
+    if (s->aa_mode < 0 || s->aa_mode > 2) return fail(RT_ERR_INVALID, "aa_mode %d", s->aa_mode);
+    return RT_OK;
+}
+
+ImageParams image_params(const rt_settings* s, int cw, int ch) {
+    ImageParams im{};
+    im.width = s->width; im.height = s->height;
+    im.x0 = s->crop_x0; im.y0 = s->crop_y0; im.cw = cw; im.ch = ch;
+    im.samples = s->samples;
+    im.s_begin = std::max(0, s->sample_begin);
+    im.s_end = s->sample_end > 0 ? std::min(s->sample_end, s->samples) : s->samples;
+    im.max_depth = s->max_depth;
+    im.aa_mode = s->aa_mode;
+    im.seedm = host_seed_mix(s->seed);
+    return im;
+}
+
+hipError_t trace(rt_scene* sc, int precision, const ImageParams& im, const Counters& c, hipStream_t st) {
+    if (im.max_depth <= 0) return hipSuccess;   // rayColor(ray, depth<=0) is 0: nothing to trace
+    if (precision == RT_PREC_F32) return launch_trace<float>(sc->s32.view, im, c, st);
+    return launch_trace<double>(sc->s64.view, im, c, st);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+const char* rt_last_error(void) { return g_error.c_str(); }
+
+int rt_device_count(int* count) {
+    if (!count) return fail(RT_ERR_INVALID, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) {
+        *count = 0;
+        return fail(RT_ERR_NO_DEVICE, "no HIP device: %s", hipGetErrorString(e));
+    }
+    *count = n;
+    return RT_OK;
+}
+
+int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out) {
+    if (!desc || !out) return fail(RT_ERR_INVALID, "NULL argument");
+    *out = nullptr;
+    if (desc->abi_version != RT_ABI_VERSION) return fail(RT_ERR_INVALID, "abi_version %d != %d", desc->abi_version, RT_ABI_VERSION);
+    if (desc->num_objects < 0 || (desc->num_objects > 0 && !desc->objects)) return fail(RT_ERR_INVALID, "objects");
+    if (desc->num_materials < 0 || (desc->num_materials > 0 && !desc->materials)) return fail(RT_ERR_INVALID, "materials");
+    if (desc->num_triangles < 0 || (desc->num_triangles > 0 && !desc->triangles)) return fail(RT_ERR_INVALID, "triangles");
+    if (desc->background < 0 || desc->background > RT_BG_NAN) return fail(RT_ERR_INVALID, "background %d", desc->background);
+    for (int i = 0; i < 512; ++i)
+        if (desc->perm[i] < 0 || desc->perm[i] > 255) return fail(RT_ERR_INVALID, "perm[%d] = %d", i, desc->perm[i]);
+    for (int i = 0; i < desc->num_materials; ++i)
+        if (desc->materials[i].type < 0 || desc->materials[i].type > RT_MAT_EMISSIVE)
+            return fail(RT_ERR_INVALID, "material %d: type %d", i, desc->materials[i].type);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RT_ERR_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= ndev) return fail(RT_ERR_INVALID, "device %d of %d", device, ndev);
+    HostScene hs;
+    std::string err;
+    if (!pack_host(*desc, hs, err)) return fail(RT_ERR_INVALID, "%s", err.c_str());
+    int rc;
+    HIP_TRY(hipSetDevice(device));
+    rt_scene* sc = new rt_scene();
+    sc->device = device;
+    sc->num_prims = hs.num_prims;
+    sc->record_bytes = hs.record_bytes;
+    if ((rc = build_device(sc->s64, hs, *desc)) || (rc = build_device(sc->s32, hs, *desc))) {
+        rt_scene_destroy(sc);
+        return rc;
+    }
+    hipError_t e = hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking);
+    for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreate(&sc->ev[k]);
+    if (e != hipSuccess) {
+        rt_scene_destroy(sc);
+        return fail(RT_ERR_DEVICE, "stream/event create: %s", hipGetErrorString(e));
+    }
+    *out = sc;
+    return RT_OK;
+}
+
+void rt_scene_destroy(rt_scene* sc) {
+    if (!sc) return;
+    (void)hipSetDevice(sc->device);
+    if (sc->stream) (void)hipStreamSynchronize(sc->stream);
+    sc->s64.release();
+    sc->s32.release();
+    sc->sum.release(); sc->mean.release(); sc->post.release(); sc->rgba.release();
+    sc->segs.release(); sc->draws.release(); sc->total.release();
+    for (auto& e : sc->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (sc->stream) (void)hipStreamDestroy(sc->stream);
+    delete sc;
+}
+
+int rt_cancel(rt_scene* sc) {
+    if (!sc) return fail(RT_ERR_INVALID, "scene is NULL");
+    sc->cancel.store(1);
+    return RT_OK;
+}
+
+int rt_render(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progress_fn progress, void* user,
+              rt_stats* stats) {
+    const double t_start = now_ms();
+    if (!sc) return fail(RT_ERR_INVALID, "scene is NULL");
+    int cw, ch;
+    int rc = check_settings(s, &cw, &ch);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(sc->device));
+    sc->cancel.store(0);
+    const size_t n = (size_t)cw * ch;
+    const bool want_segs = out && out->segments, want_draws = out && out->draws;
+    HIP_TRY(sc->sum.ensure(3 * n));
+    HIP_TRY(sc->total.ensure(1));
+    HIP_TRY(hipMemsetAsync(sc->sum.p, 0, 3 * n * sizeof(double), sc->stream));
+    HIP_TRY(hipMemsetAsync(sc->total.p, 0, sizeof(unsigned long long), sc->stream));
+    Counters c{sc->sum.p, nullptr, nullptr, sc->total.p};
+    if (want_segs) {
+        HIP_TRY(sc->segs.ensure(n));
+        HIP_TRY(hipMemsetAsync(sc->segs.p, 0, n * sizeof(uint32_t), sc->stream));
+        c.segs = sc->segs.p;
+    }
+    if (want_draws) {
+        HIP_TRY(sc->draws.ensure(n));
+        HIP_TRY(hipMemsetAsync(sc->draws.p, 0, n * sizeof(uint32_t), sc->stream));
+        c.draws = sc->draws.p;
+    }
+    ImageParams im = image_params(s, cw, ch);
+    const int s0 = im.s_begin, s1 = im.s_end;
+    const int batch = s->batch_samples > 0 ? s->batch_samples : std::max(1, s1 - s0);
+    double kernel_ms = 0;
+    for (int b = s0; b < s1; b += batch) {
+        ImageParams bi = im;
+        bi.s_begin = b;
+        bi.s_end = std::min(s1, b + batch);
+        HIP_TRY(hipEventRecord(sc->ev[0], sc->stream));
+        HIP_TRY(trace(sc, s->precision, bi, c, sc->stream));
+        HIP_TRY(hipEventRecord(sc->ev[1], sc->stream));
+        HIP_TRY(hipEventSynchronize(sc->ev[1]));
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, sc->ev[0], sc->ev[1]));
+        kernel_ms += ms;
+        if (progress && bi.s_end < s1) {
+            if (progress((double)(bi.s_end - s0) / (double)(s1 - s0), user)) sc->cancel.store(1);
+        }
+        if (sc->cancel.load()) return fail(RT_ERR_CANCELLED, "render cancelled after %d samples", bi.s_end);
+    }
+    FinalizeParams fp{(int)n, s->samples, s->tone_map, s->exposure, s->gamma};
+    const bool want_mean = out && out->mean, want_post = out && out->post, want_rgba = out && out->rgba8;
+    if (want_mean) HIP_TRY(sc->mean.ensure(3 * n));
+    if (want_post) HIP_TRY(sc->post.ensure(4 * n));
+    if (want_rgba) HIP_TRY(sc->rgba.ensure(4 * n));
+    HIP_TRY(hipEventRecord(sc->ev[2], sc->stream));
+    HIP_TRY(launch_finalize(fp, sc->sum.p, want_mean ? sc->mean.p : nullptr, want_post ? sc->post.p : nullptr,
+                            want_rgba ? sc->rgba.p : nullptr, sc->stream));
+    HIP_TRY(hipEventRecord(sc->ev[3], sc->stream));
+    if (want_mean) HIP_TRY(hipMemcpyAsync(out->mean, sc->mean.p, 3 * n * sizeof(double), hipMemcpyDeviceToHost, sc->stream));
+    if (want_post) HIP_TRY(hipMemcpyAsync(out->post, sc->post.p, 4 * n * sizeof(float), hipMemcpyDeviceToHost, sc->stream));
+    if (want_rgba) HIP_TRY(hipMemcpyAsync(out->rgba8, sc->rgba.p, 4 * n, hipMemcpyDeviceToHost, sc->stream));
+    if (want_segs) HIP_TRY(hipMemcpyAsync(out->segments, sc->segs.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, sc->stream));
+    if (want_draws) HIP_TRY(hipMemcpyAsync(out->draws, sc->draws.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, sc->stream));
+    unsigned long long total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, sc->total.p, sizeof total, hipMemcpyDeviceToHost, sc->stream));
+    HIP_TRY(hipStreamSynchronize(sc->stream));
+    if (stats) {
+        float fms = 0;
+        HIP_TRY(hipEventElapsedTime(&fms, sc->ev[2], sc->ev[3]));
+        stats->kernel_ms = kernel_ms;
+        stats->finalize_ms = fms;
+        stats->samples = (uint64_t)n * (uint64_t)std::max(0, s1 - s0);
+        stats->segments = total;
+        stats->prim_tests = total * (uint64_t)sc->num_prims;
+        stats->algorithmic_bytes = (double)total * sc->record_bytes + 12.0 * (double)n;
+        stats->wall_ms = now_ms() - t_start;
+    }
+    return RT_OK;
+}
+
+int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip_stream, int sync, rt_stats* stats) {
+    const double t_start = now_ms();
+    if (!sc || !d_sum) return fail(RT_ERR_INVALID, "NULL argument");
+    int cw, ch;
+    int rc = check_settings(s, &cw, &ch);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(sc->device));
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : sc->stream;
+    HIP_TRY(sc->total.ensure(1));
+    HIP_TRY(hipMemsetAsync(sc->total.p, 0, sizeof(unsigned long long), st));
+    ImageParams im = image_params(s, cw, ch);
+    Counters c{d_sum, nullptr, nullptr, sc->total.p};
+    HIP_TRY(hipEventRecord(sc->ev[0], st));
+    HIP_TRY(trace(sc, s->precision, im, c, st));
+    HIP_TRY(hipEventRecord(sc->ev[1], st));
+    if (sync || stats) {
+        unsigned long long total = 0;
+        HIP_TRY(hipMemcpyAsync(&total, sc->total.p, sizeof total, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (stats) {
+            float ms = 0;
+            HIP_TRY(hipEventElapsedTime(&ms, sc->ev[0], sc->ev[1]));
+            const size_t n = (size_t)cw * ch;
+            stats->kernel_ms = ms;
+            stats->finalize_ms = 0;
+            stats->samples = (uint64_t)n * (uint64_t)std::max(0, im.s_end - im.s_begin);
+            stats->segments = total;
+            stats->prim_tests = total * (uint64_t)sc->num_prims;
+            stats->algorithmic_bytes = (double)total * sc->record_bytes + 12.0 * (double)n;
+            stats->wall_ms = now_ms() - t_start;
+        }
+    }
+    return RT_OK;
+}
+
+int rt_finalize_device(const rt_settings* s, const double* d_sum, double* d_mean, float* d_post, uint8_t* d_rgba8,
+                       void* hip_stream) {
+    int cw, ch;
+    int rc = check_settings(s, &cw, &ch);
+    if (rc) return rc;
+    if (!d_sum) return fail(RT_ERR_INVALID, "d_sum is NULL");
+    FinalizeParams fp{cw * ch, s->samples, s->tone_map, s->exposure, s->gamma};
+    HIP_TRY(launch_finalize(fp, d_sum, d_mean, d_post, d_rgba8, (hipStream_t)hip_stream));
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -81,7 +81,7 @@ typedef struct rt_material_desc {
     double roughness;      /* Metal: already Math.min(roughness, 1) (materials.js:33) */
     double ior;            /* Dielectric refractionIndex */
     double emission[3];    /* Emissive: color.mul(intensity) (materials.js:95), evaluated in double */
-} rt_material_desc;        /* 80 bytes */
+} rt_material_desc;        /* 72 bytes */
 
 typedef struct rt_object_desc {
     int32_t type;          /* rt_object_type */
@@ -155,7 +155,7 @@ typedef struct rt_stats {
     uint64_t samples;            /* pixels x samples traced */
     uint64_t segments;           /* world.hit calls (ray segments) */
     uint64_t prim_tests;         /* segments x primitives tested (brute force) */
-    double algorithmic_bytes;    /* prim_tests x record bytes (+ framebuffer) */
+    double algorithmic_bytes;    /* segments x sum of primitive record bytes + 12 B/pixel framebuffer */
 } rt_stats;
 
 typedef struct rt_scene rt_scene;   /* opaque: scene resident in HBM of one device */

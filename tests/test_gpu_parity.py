@@ -1,0 +1,150 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden fixtures and the
+oracle.  Tolerances (BASELINE.json north_star: <= 1e-3 per-channel RMS vs the JS reference):
+  * f64 mode  — same arithmetic as the JS: segment counts and RNG draw counts per pixel must be
+                identical (every path decision matches), linear means within 1e-12 relative
+                (only the forward throughput product's rounding differs from the recursion's),
+                RGBA8 identical;
+  * f32 mode  — per-channel RMS of post-gamma values <= 1e-3 where the survey's budget applies
+                (>= 64 spp), looser bounds documented per case at low spp.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import golden_cases as gc
+from blenderraytracer_amd import capi
+from blenderraytracer_amd.renderer import GpuRayTracer
+from blenderraytracer_amd.scene import load_scene_json
+from oracle import binding
+
+pytestmark = pytest.mark.gpu
+
+WANT = ("mean", "segments", "draws")
+
+
+def rel_err(a, b):
+    ok = ~(np.isnan(a) & np.isnan(b))
+    return float(np.max(np.abs(a[ok] - b[ok]) / np.maximum(1.0, np.abs(b[ok])))) if ok.any() else 0.0
+
+
+@pytest.mark.parametrize("case", gc.case_names())
+def test_f64_matches_reference(gpu, case):
+    rt, c = gc.tracer_for(case, precision=capi.RT_PREC_F64)
+    r = rt.render(crop=c["crop"], want=WANT)
+    lin = gc.load_array(case, "linear")
+    assert np.array_equal(np.isnan(r["mean"]), np.isnan(lin))
+    assert np.array_equal(r["segments"], gc.load_array(case, "segs")), "world.hit count per pixel differs"
+    assert np.array_equal(r["draws"], gc.load_array(case, "draws")), "RNG draws per pixel differ"
+    assert rel_err(r["mean"], lin) <= 1e-12
+    rgba = gc.load_array(case, "rgba8")
+    assert np.mean(r["rgba8"] == rgba) >= 0.9999, "RGBA8 differs"
+    post = gc.load_array(case, "post")
+    ok = ~np.isnan(post)
+    assert np.max(np.abs(r["post"][..., :3][ok] - post[ok]), initial=0) <= 1e-6   # float32 storage
+    rt.close()
+
+
+# f32 fast mode: RMS of post-gamma output vs the reference.  At these low sample counts a single
+# flipped path decision moves a pixel by up to 1/spp, so the bounds are per case; the north-star
+# budget (1e-3) is asserted on the 512-spp RTOW crop.
+F32_RMS = {"cfg3_rtow_crop_512spp": 1e-3}
+
+
+@pytest.mark.parametrize("case", gc.case_names())
+def test_f32_rms(gpu, case):
+    rt, c = gc.tracer_for(case, precision=capi.RT_PREC_F32)
+    r = rt.render(crop=c["crop"])
+    post = gc.load_array(case, "post")
+    ok = ~np.isnan(post)
+    assert np.array_equal(np.isnan(r["post"][..., :3]), ~ok)
+    rms = float(np.sqrt(np.mean((r["post"][..., :3][ok] - post[ok]) ** 2))) if ok.any() else 0.0
+    print(f"{case}: f32 post-gamma RMS {rms:.2e}")
+    assert rms <= F32_RMS.get(case, 3e-2)
+    rt.close()
+
+
+def _rtow(w, h, spp, precision=capi.RT_PREC_F64, seed=1234):
+    rt = GpuRayTracer(w, h, seed=seed, precision=precision)
+    assert rt.load_from_json(load_scene_json("rtow.json"))
+    rt.update_render_settings({"maxBounces": 5, "samples": spp})
+    return rt
+
+
+def test_f64_matches_oracle_rtow(gpu):
+    rt = _rtow(160, 90, 16)
+    r = rt.render(want=WANT)
+    o = binding.render(rt.packed(), rt.settings())
+    assert np.array_equal(r["segments"], o["segments"]) and np.array_equal(r["draws"], o["draws"])
+    assert rel_err(r["mean"], o["mean"]) <= 1e-12
+    assert np.array_equal(r["rgba8"], o["rgba8"])
+
+
+def test_batching_is_bit_exact(gpu):
+    """Sample batches continue each pixel's running sum in order: identical bits to one launch."""
+    rt = _rtow(96, 54, 12)
+    full = rt.render(want=("mean",))["mean"]
+    batched = rt.render(want=("mean",), batch_samples=5)["mean"]
+    assert np.array_equal(full, batched)
+
+
+def test_crop_is_bit_exact_window_of_full(gpu):
+    rt = _rtow(128, 72, 6)
+    full = rt.render(want=("mean",))["mean"]
+    crop = rt.render(want=("mean",), crop=(37, 11, 50, 29))["mean"]
+    assert np.array_equal(full[11:40, 37:87], crop)
+
+
+def test_deterministic_and_progress(gpu):
+    rt = _rtow(64, 36, 8)
+    seen = []
+    a = rt.render(want=("mean",), batch_samples=2, on_progress=lambda f: seen.append(f) and False)["mean"]
+    b = rt.render(want=("mean",))["mean"]
+    assert np.array_equal(a, b)
+    assert seen and seen[-1] == 1.0 and all(x <= y for x, y in zip(seen, seen[1:]))
+
+
+def test_cancel_via_progress(gpu):
+    rt = _rtow(64, 36, 8)
+    with pytest.raises(RuntimeError, match="CANCELLED"):
+        rt.render(batch_samples=2, on_progress=lambda f: True)
+
+
+def test_max_depth_zero_is_black(gpu):
+    rt = _rtow(32, 18, 4)
+    rt.max_bounces = -1        # truthy in JS: rayColor(ray, -1) returns 0 immediately
+    r = rt.render(want=("mean", "segments"))
+    assert np.all(r["mean"] == 0) and np.all(r["segments"] == 0)
+
+
+def test_trace_device_sample_split(gpu):
+    """Sample-range sharding (the multi-GPU path): partial sums over [0,k) and [k,S) add up."""
+    import torch
+    rt = _rtow(80, 45, 10)
+    lib = capi.load_library()
+    scene = rt.scene_handle()
+    n = 80 * 45
+    sums = []
+    for rng in ((0, 10), (0, 4), (4, 10)):
+        buf = torch.zeros(n * 3, dtype=torch.float64, device="cuda")
+        st = rt.settings(sample_range=rng)
+        torch.cuda.synchronize()
+        capi.check(lib.rt_trace_device(scene, C.byref(st), C.c_void_p(buf.data_ptr()), None, 1, None))
+        sums.append(buf.cpu().numpy())
+    full, a, b = sums
+    assert np.allclose(a + b, full, rtol=1e-13, atol=0)
+
+
+def test_full_resolution_config3_properties(gpu):
+    """Config 3 at its full 1920x1080 size (2 spp): finite, deterministic, windows match the oracle."""
+    rt = _rtow(1920, 1080, 2, seed=17)
+    r1 = rt.render(want=("mean", "segments"))
+    r2 = rt.render(want=("mean",))
+    assert np.all(np.isfinite(r1["mean"]))
+    assert np.array_equal(r1["mean"], r2["mean"])
+    for (x0, y0) in ((0, 0), (950, 530), (1904, 1064)):
+        o = binding.render(rt.packed(), rt.settings(crop=(x0, y0, 16, 16)))
+        assert np.array_equal(o["segments"], r1["segments"][y0:y0 + 16, x0:x0 + 16])
+        assert rel_err(r1["mean"][y0:y0 + 16, x0:x0 + 16], o["mean"]) <= 1e-12
+    seg_per_sample = r1["segments"].sum() / (1920 * 1080 * 2)
+    assert 1.5 < seg_per_sample < 4.0
