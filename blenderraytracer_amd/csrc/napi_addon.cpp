@@ -1,0 +1,374 @@
+// napi_addon.cpp — Node N-API binding of librt_hip.so (rt_napi.node).
+//
+// The JS host (blenderraytracer_amd/js/gpu-ray-tracer.mjs) keeps the reference's RayTracer surface
+// and calls into this addon for the part under RayTracer.render (js/ray-tracer.js:166-281):
+//   createScene(desc, device)          -> External   (rt_scene_create: scene copied into HBM)
+//   render(scene, settings, progress?) -> Promise<{mean, post, rgba8, segments?, draws?, stats}>
+//                                         (rt_render on a libuv worker thread: the event loop stays live)
+//   cancel(scene)                      -> rt_cancel (polled between sample batches)
+//   destroyScene(scene), deviceCount(), abiVersion()
+// Progress reaches JS through a napi_threadsafe_function; C errors reject the Promise with
+// Error(rt_last_error()).  Built with plain g++ against node_api.h (no node-gyp).
+#define NAPI_VERSION 6
+#include <node_api.h>
+
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rt_hip.h"
+
+namespace {
+
+#define NAPI_OK(call)                                                       \
+    do {                                                                    \
+        if ((call) != napi_ok) {                                            \
+            napi_throw_error(env, nullptr, "N-API call failed: " #call);   \
+            return nullptr;                                                 \
+        }                                                                   \
+    } while (0)
+
+napi_value throw_err(napi_env env, const std::string& msg) {
+    napi_throw_error(env, nullptr, msg.c_str());
+    return nullptr;
+}
+
+bool get_prop(napi_env env, napi_value obj, const char* key, napi_value* out) {
+    bool has = false;
+    if (napi_has_named_property(env, obj, key, &has) != napi_ok || !has) return false;
+    if (napi_get_named_property(env, obj, key, out) != napi_ok) return false;
+    napi_valuetype t;
+    napi_typeof(env, *out, &t);
+    return t != napi_undefined && t != napi_null;
+}
+
+double get_num(napi_env env, napi_value obj, const char* key, double dflt) {
+    napi_value v;
+    double d = dflt;
+    if (get_prop(env, obj, key, &v)) napi_get_value_double(env, v, &d);
+    return d;
+}
+
+// Raw bytes of a TypedArray / ArrayBuffer / DataView property.
+bool get_bytes(napi_env env, napi_value obj, const char* key, void** data, size_t* bytes) {
+    napi_value v;
+    *data = nullptr;
+    *bytes = 0;
+    if (!get_prop(env, obj, key, &v)) return false;
+    bool is;
+    if (napi_is_typedarray(env, v, &is) == napi_ok && is) {
+        napi_typedarray_type t;
+        size_t len, off;
+        napi_value ab;
+        void* p;
+        napi_get_typedarray_info(env, v, &t, &len, &p, &ab, &off);
+        size_t el = (t == napi_float64_array || t == napi_bigint64_array || t == napi_biguint64_array) ? 8
+                    : (t == napi_int32_array || t == napi_uint32_array || t == napi_float32_array) ? 4
+                    : (t == napi_int16_array || t == napi_uint16_array) ? 2 : 1;
+        *data = p;
+        *bytes = len * el;
+        return true;
+    }
+    if (napi_is_arraybuffer(env, v, &is) == napi_ok && is) {
+        napi_get_arraybuffer_info(env, v, data, bytes);
+        return true;
+    }
+    if (napi_is_dataview(env, v, &is) == napi_ok && is) {
+        napi_value ab;
+        size_t off;
+        napi_get_dataview_info(env, v, bytes, data, &ab, &off);
+        return true;
+    }
+    return false;
+}
+
+// The External owns a SceneBox: destroyScene() frees the device scene eagerly, the GC finalizer
+// frees whatever is left; one render may be in flight per scene (rt_hip.h threading rule).
+struct SceneBox {
+    rt_scene* sc = nullptr;
+    bool busy = false;
+};
+
+void scene_finalize(napi_env, void* data, void*) {
+    SceneBox* box = static_cast<SceneBox*>(data);
+    if (box->sc) rt_scene_destroy(box->sc);
+    delete box;
+}
+
+SceneBox* get_box(napi_env env, napi_value v) {
+    void* p = nullptr;
+    napi_valuetype t;
+    if (napi_typeof(env, v, &t) != napi_ok || t != napi_external) return nullptr;
+    if (napi_get_value_external(env, v, &p) != napi_ok) return nullptr;
+    return static_cast<SceneBox*>(p);
+}
+
+// createScene(desc, device): desc holds the rt_scene_desc records as typed arrays (layout: rt_hip.h)
+napi_value create_scene(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    if (argc < 1) return throw_err(env, "createScene(desc, device)");
+    napi_value d = argv[0];
+    int32_t device = 0;
+    if (argc > 1) napi_get_value_int32(env, argv[1], &device);
+    rt_scene_desc desc;
+    std::memset(&desc, 0, sizeof desc);
+    desc.abi_version = RT_ABI_VERSION;
+    void* p;
+    size_t n;
+    if (get_bytes(env, d, "objects", &p, &n)) {
+        desc.objects = static_cast<const rt_object_desc*>(p);
+        desc.num_objects = (int32_t)(n / sizeof(rt_object_desc));
+    }
+    if (get_bytes(env, d, "materials", &p, &n)) {
+        desc.materials = static_cast<const rt_material_desc*>(p);
+        desc.num_materials = (int32_t)(n / sizeof(rt_material_desc));
+    }
+    if (get_bytes(env, d, "triangles", &p, &n)) {
+        desc.triangles = static_cast<const double*>(p);
+        desc.num_triangles = (int32_t)(n / (12 * sizeof(double)));
+    }
+    if (!get_bytes(env, d, "camera", &p, &n) || n != 22 * sizeof(double))
+        return throw_err(env, "desc.camera must be a Float64Array(22): origin, lowerLeft, horizontal, vertical, u, v, w, lensRadius");
+    const double* c = static_cast<const double*>(p);
+    std::memcpy(desc.camera.origin, c + 0, 24);
+    std::memcpy(desc.camera.lower_left, c + 3, 24);
+    std::memcpy(desc.camera.horizontal, c + 6, 24);
+    std::memcpy(desc.camera.vertical, c + 9, 24);
+    std::memcpy(desc.camera.u, c + 12, 24);
+    std::memcpy(desc.camera.v, c + 15, 24);
+    std::memcpy(desc.camera.w, c + 18, 24);
+    desc.camera.lens_radius = c[21];
+    desc.camera.type = (int32_t)get_num(env, d, "cameraType", RT_CAM_PERSPECTIVE);
+    desc.background = (int32_t)get_num(env, d, "background", RT_BG_GRADIENT);
+    desc.sky_intensity = get_num(env, d, "skyIntensity", 1.0);
+    if (get_bytes(env, d, "solidColor", &p, &n) && n == 3 * sizeof(double)) std::memcpy(desc.solid_color, p, 24);
+    if (!get_bytes(env, d, "perm", &p, &n) || n != 512 * sizeof(int32_t))
+        return throw_err(env, "desc.perm must be an Int32Array(512) (World.cloudNoise.p)");
+    std::memcpy(desc.perm, p, sizeof desc.perm);
+    rt_scene* sc = nullptr;
+    if (rt_scene_create(&desc, device, &sc) != RT_OK) return throw_err(env, std::string("rt_scene_create: ") + rt_last_error());
+    SceneBox* box = new SceneBox();
+    box->sc = sc;
+    napi_value ext;
+    NAPI_OK(napi_create_external(env, box, scene_finalize, nullptr, &ext));
+    return ext;
+}
+
+struct RenderJob {
+    napi_async_work work = nullptr;
+    napi_deferred deferred = nullptr;
+    napi_threadsafe_function tsfn = nullptr;
+    napi_ref scene_ref = nullptr;   // keeps the External (and its rt_scene) alive while rendering
+    SceneBox* box = nullptr;
+    rt_scene* scene = nullptr;
+    rt_settings st{};
+    size_t n = 0;
+    bool want_mean = false, want_counts = false;
+    std::vector<double> mean;
+    std::vector<float> post;
+    std::vector<uint8_t> rgba;
+    std::vector<uint32_t> segs, draws;
+    rt_stats stats{};
+    int status = 0;
+    std::string error;
+    std::atomic<int> cancel_from_js{0};
+};
+
+void call_progress(napi_env env, napi_value js_cb, void*, void* data) {
+    double* frac = static_cast<double*>(data);
+    if (env && js_cb) {
+        napi_value arg, undef;
+        napi_create_double(env, *frac, &arg);
+        napi_get_undefined(env, &undef);
+        napi_call_function(env, undef, js_cb, 1, &arg, nullptr);
+    }
+    delete frac;
+}
+
+int progress_hook(double fraction, void* user) {
+    RenderJob* job = static_cast<RenderJob*>(user);
+    if (job->tsfn) napi_call_threadsafe_function(job->tsfn, new double(fraction), napi_tsfn_nonblocking);
+    return job->cancel_from_js.load();
+}
+
+void execute(napi_env, void* data) {
+    RenderJob* job = static_cast<RenderJob*>(data);
+    rt_output out{};
+    job->post.resize(job->n * 4);
+    job->rgba.resize(job->n * 4);
+    out.post = job->post.data();
+    out.rgba8 = job->rgba.data();
+    if (job->want_mean) {
+        job->mean.resize(job->n * 3);
+        out.mean = job->mean.data();
+    }
+    if (job->want_counts) {
+        job->segs.resize(job->n);
+        job->draws.resize(job->n);
+        out.segments = job->segs.data();
+        out.draws = job->draws.data();
+    }
+    job->status = rt_render(job->scene, &job->st, &out, progress_hook, job, &job->stats);
+    if (job->status != RT_OK) job->error = rt_last_error();
+}
+
+template <class T>
+napi_value to_typed(napi_env env, const std::vector<T>& v, napi_typedarray_type t) {
+    napi_value ab, arr;
+    void* p = nullptr;
+    napi_create_arraybuffer(env, v.size() * sizeof(T), &p, &ab);
+    if (!v.empty()) std::memcpy(p, v.data(), v.size() * sizeof(T));
+    napi_create_typedarray(env, t, v.size(), ab, 0, &arr);
+    return arr;
+}
+
+void complete(napi_env env, napi_status, void* data) {
+    RenderJob* job = static_cast<RenderJob*>(data);
+    if (job->tsfn) napi_release_threadsafe_function(job->tsfn, napi_tsfn_release);
+    if (job->status != RT_OK) {
+        napi_value msg, err, code;
+        napi_create_string_utf8(env, job->error.c_str(), NAPI_AUTO_LENGTH, &msg);
+        napi_create_error(env, nullptr, msg, &err);
+        napi_create_int32(env, job->status, &code);
+        napi_set_named_property(env, err, "status", code);
+        napi_reject_deferred(env, job->deferred, err);
+    } else {
+        napi_value res, stats, v;
+        napi_create_object(env, &res);
+        napi_set_named_property(env, res, "post", to_typed(env, job->post, napi_float32_array));
+        napi_set_named_property(env, res, "rgba8", to_typed(env, job->rgba, napi_uint8_clamped_array));
+        if (job->want_mean) napi_set_named_property(env, res, "mean", to_typed(env, job->mean, napi_float64_array));
+        if (job->want_counts) {
+            napi_set_named_property(env, res, "segments", to_typed(env, job->segs, napi_uint32_array));
+            napi_set_named_property(env, res, "draws", to_typed(env, job->draws, napi_uint32_array));
+        }
+        napi_create_object(env, &stats);
+        const struct { const char* k; double v; } fields[] = {
+            {"kernelMs", job->stats.kernel_ms}, {"finalizeMs", job->stats.finalize_ms}, {"wallMs", job->stats.wall_ms},
+            {"samples", (double)job->stats.samples}, {"segments", (double)job->stats.segments},
+            {"primTests", (double)job->stats.prim_tests}, {"algorithmicBytes", job->stats.algorithmic_bytes}};
+        for (const auto& f : fields) {
+            napi_create_double(env, f.v, &v);
+            napi_set_named_property(env, stats, f.k, v);
+        }
+        napi_set_named_property(env, res, "stats", stats);
+        napi_resolve_deferred(env, job->deferred, res);
+    }
+    job->box->busy = false;
+    napi_delete_reference(env, job->scene_ref);
+    napi_delete_async_work(env, job->work);
+    delete job;
+}
+
+// render(scene, settings, onProgress?) -> Promise
+napi_value render(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    if (argc < 2) return throw_err(env, "render(scene, settings, onProgress?)");
+    SceneBox* box = get_box(env, argv[0]);
+    if (!box || !box->sc) return throw_err(env, "render: first argument is not a live scene");
+    if (box->busy) return throw_err(env, "render: a render is already in flight on this scene");
+    napi_value s = argv[1];
+    RenderJob* job = new RenderJob();
+    job->box = box;
+    job->scene = box->sc;
+    rt_settings& st = job->st;
+    st.width = (int32_t)get_num(env, s, "width", 0);
+    st.height = (int32_t)get_num(env, s, "height", 0);
+    st.samples = (int32_t)get_num(env, s, "samples", 4);
+    st.max_depth = (int32_t)get_num(env, s, "maxDepth", 5);
+    st.aa_mode = (int32_t)get_num(env, s, "aaMode", RT_AA_SUPERSAMPLING);
+    st.tone_map = (int32_t)get_num(env, s, "toneMap", RT_TM_REINHARD);
+    st.exposure = get_num(env, s, "exposure", 1.0);
+    st.gamma = get_num(env, s, "gamma", 2.2);
+    st.seed = (uint32_t)get_num(env, s, "seed", 0);
+    st.sample_begin = (int32_t)get_num(env, s, "sampleBegin", 0);
+    st.sample_end = (int32_t)get_num(env, s, "sampleEnd", 0);
+    st.crop_x0 = (int32_t)get_num(env, s, "cropX0", 0);
+    st.crop_y0 = (int32_t)get_num(env, s, "cropY0", 0);
+    st.crop_w = (int32_t)get_num(env, s, "cropW", 0);
+    st.crop_h = (int32_t)get_num(env, s, "cropH", 0);
+    st.precision = (int32_t)get_num(env, s, "precision", RT_PREC_F64);
+    st.batch_samples = (int32_t)get_num(env, s, "batchSamples", 0);
+    job->want_mean = get_num(env, s, "wantMean", 0) != 0;
+    job->want_counts = get_num(env, s, "wantCounts", 0) != 0;
+    const int cw = st.crop_w > 0 ? st.crop_w : st.width, ch = st.crop_h > 0 ? st.crop_h : st.height;
+    if (cw <= 0 || ch <= 0) {
+        delete job;
+        return throw_err(env, "render: width/height must be positive");
+    }
+    job->n = (size_t)cw * ch;
+    napi_value promise, name;
+    NAPI_OK(napi_create_promise(env, &job->deferred, &promise));
+    NAPI_OK(napi_create_reference(env, argv[0], 1, &job->scene_ref));
+    NAPI_OK(napi_create_string_utf8(env, "rt_render", NAPI_AUTO_LENGTH, &name));
+    if (argc > 2) {
+        napi_valuetype t;
+        napi_typeof(env, argv[2], &t);
+        if (t == napi_function)
+            NAPI_OK(napi_create_threadsafe_function(env, argv[2], nullptr, name, 0, 1, nullptr, nullptr, nullptr,
+                                                    call_progress, &job->tsfn));
+    }
+    NAPI_OK(napi_create_async_work(env, nullptr, name, execute, complete, job, &job->work));
+    NAPI_OK(napi_queue_async_work(env, job->work));
+    box->busy = true;
+    return promise;
+}
+
+napi_value cancel(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    SceneBox* box = argc ? get_box(env, argv[0]) : nullptr;
+    if (!box) return throw_err(env, "cancel(scene)");
+    if (box->sc) rt_cancel(box->sc);
+    return nullptr;
+}
+
+napi_value destroy_scene(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    SceneBox* box = argc ? get_box(env, argv[0]) : nullptr;
+    if (!box) return throw_err(env, "destroyScene(scene)");
+    if (box->busy) return throw_err(env, "destroyScene: a render is in flight");
+    if (box->sc) rt_scene_destroy(box->sc);
+    box->sc = nullptr;
+    return nullptr;
+}
+
+napi_value device_count(napi_env env, napi_callback_info) {
+    int n = 0;
+    rt_device_count(&n);
+    napi_value v;
+    napi_create_int32(env, n, &v);
+    return v;
+}
+
+napi_value abi_version(napi_env env, napi_callback_info) {
+    napi_value v;
+    napi_create_int32(env, rt_abi_version(), &v);
+    return v;
+}
+
+napi_value init(napi_env env, napi_value exports) {
+    const napi_property_descriptor props[] = {
+        {"createScene", nullptr, create_scene, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"render", nullptr, render, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"cancel", nullptr, cancel, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"destroyScene", nullptr, destroy_scene, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"deviceCount", nullptr, device_count, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"abiVersion", nullptr, abi_version, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+    };
+    napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
+    return exports;
+}
+
+}  // namespace
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

@@ -1,0 +1,163 @@
+// GpuRayTracer — drop-in for the reference's RayTracer.render (js/ray-tracer.js:166-281) on MI355X.
+//
+// Two ways to use it:
+//   1. installGpuRender(rayTracer, opts): replaces render() on an instance of the REFERENCE's own
+//      RayTracer class.  Everything else (loadFromJSON, presets, updateCamera, UI) stays the
+//      reference's code; render() packs this.world / this.camera (pack.mjs), traces on the GPU
+//      through rt_napi.node -> librt_hip.so, and fills this.imageData like the reference does.
+//   2. new GpuRayTracer(canvasOrSize, opts): a DOM-free RayTracer twin for Node (bench, tests, GPU
+//      box) with the reference's loadFromJSON / updateRenderSettings / updateBackground semantics
+//      restated in scene-model.mjs.
+// Randomness: Math.random is replaced by the keyed RNG (keyed-rng.mjs); opts.seed selects it.
+import { createRequire } from 'module';
+import path from 'path';
+import { fileURLToPath } from 'url';
+import { packScene } from './pack.mjs';
+import { Vec3, BG, defaultScene, loadFromJSON, setupCamera, permutation } from './scene-model.mjs';
+
+const HERE = path.dirname(fileURLToPath(import.meta.url));
+let native = null;
+
+export function loadNative() {
+    if (!native) {
+        const require = createRequire(import.meta.url);
+        const p = process.env.RT_NAPI_ADDON || path.join(HERE, '..', 'lib', 'rt_napi.node');
+        native = require(p);   // throws if the addon (or librt_hip.so) is missing: no CPU fallback
+    }
+    return native;
+}
+
+export const AA = { supersampling: 0, stochastic: 1 };            // anything else: pixel centre (2)
+export const TONE = { aces: 1, linear: 2 };                        // anything else: reinhard (0)
+export const PRECISION = { f64: 0, f32: 1 };
+
+// rt_settings from RayTracer fields (ray-tracer.js:23-33, :201, :125-161)
+export function settingsOf(rt, opts = {}) {
+    return {
+        width: rt.width, height: rt.height,
+        samples: rt.antiAliasing === 'none' ? 1 : rt.samples,
+        maxDepth: rt.maxBounces,
+        aaMode: AA[rt.antiAliasing] !== undefined ? AA[rt.antiAliasing] : 2,
+        toneMap: TONE[rt.toneMapping] !== undefined ? TONE[rt.toneMapping] : 0,
+        exposure: rt.exposure, gamma: rt.gamma,
+        seed: (opts.seed || 0) >>> 0,
+        precision: PRECISION[opts.precision || 'f64'],
+        batchSamples: opts.batchSamples || 0,
+        cropX0: opts.crop ? opts.crop[0] : 0, cropY0: opts.crop ? opts.crop[1] : 0,
+        cropW: opts.crop ? opts.crop[2] : 0, cropH: opts.crop ? opts.crop[3] : 0,
+        wantMean: opts.wantMean ? 1 : 0, wantCounts: opts.wantCounts ? 1 : 0,
+    };
+}
+
+const isCancelled = () => typeof window !== 'undefined' && window && window.renderCancelled;
+
+// The GPU body of render(): trace, epilogue and readback; returns the native result (or null when
+// cancelled, like the reference which then stops silently, ray-tracer.js:256,264).
+export async function gpuRender(rt, onProgress, opts = {}) {
+    const nat = loadNative();
+    const scene = nat.createScene(packScene(rt.world, rt.camera), opts.device || 0);
+    try {
+        const res = await nat.render(scene, settingsOf(rt, opts), (f) => {
+            if (onProgress) onProgress(f);
+            if (isCancelled()) nat.cancel(scene);
+        });
+        return res;
+    } catch (e) {
+        if (e && e.status === -4) return null;                    // RT_ERR_CANCELLED
+        throw e;
+    } finally {
+        nat.destroyScene(scene);
+    }
+}
+
+function blit(rt, res) {
+    // ray-tracer.js:215-252: RGBA8 top-down row-major, alpha 255 (computed on the GPU)
+    rt.imageData.data.set(res.rgba8);
+    rt.floatData = res.post;
+    if (rt.ctx && rt.ctx.putImageData) rt.ctx.putImageData(rt.imageData, 0, 0);
+}
+
+function checkSupported(rt) {
+    if (rt.denoising) throw new Error('denoising is not yet on the GPU path (SURVEY §8f rank 1)');
+}
+
+// Option 1: swap the render() of a reference RayTracer instance for the GPU path.
+export function installGpuRender(rayTracer, opts = {}) {
+    rayTracer.render = async function render(onProgress) {
+        checkSupported(this);
+        const res = await gpuRender(this, onProgress, opts);
+        if (!res) return;
+        blit(this, res);
+        this.lastStats = res.stats;
+        if (onProgress) onProgress(1.0);
+    };
+    return rayTracer;
+}
+
+// Option 2: the DOM-free twin.
+export class GpuRayTracer {
+    constructor(canvas, opts = {}) {
+        this.canvas = canvas && canvas.getContext ? canvas : null;
+        this.ctx = this.canvas ? this.canvas.getContext('2d') : null;
+        this.width = canvas.width;
+        this.height = canvas.height;
+        this.opts = opts;
+        this.imageData = this.ctx ? this.ctx.createImageData(this.width, this.height) : { width: this.width, height: this.height, data: new Uint8ClampedArray(this.width * this.height * 4) };
+        this.maxBounces = 5; this.samples = 4; this.gamma = 2.2; this.exposure = 1.0;
+        this.toneMapping = 'reinhard'; this.antiAliasing = 'supersampling';
+        this.denoising = false; this.denoiseStrength = 0.5;
+        const d = defaultScene(this.width, this.height, permutation(opts.seed || 0));
+        this.world = d.world;
+        this.camera = d.camera;
+    }
+
+    loadFromJSON(json) {                                             // ray-tracer.js:305-334
+        try {
+            const r = loadFromJSON(json, this.width, this.height, permutation(this.opts.seed || 0));
+            this.world = r.world;
+            if (r.camera) this.camera = r.camera;
+            if (r.newDimensions) this.resizeCanvas(r.newDimensions.width, r.newDimensions.height);
+            return true;
+        } catch (e) {
+            return false;
+        }
+    }
+
+    resizeCanvas(width, height) {                                    // ray-tracer.js:598-614
+        this.width = width; this.height = height;
+        if (this.canvas) { this.canvas.width = width; this.canvas.height = height; }
+        this.imageData = { width, height, data: new Uint8ClampedArray(width * height * 4) };
+        if (this.camera) this.camera = setupCamera(this.camera, width, height);
+    }
+
+    updateRenderSettings(p) {                                        // ray-tracer.js:554-566
+        this.maxBounces = p.maxBounces || 5;
+        this.samples = p.samples || 4;
+        this.gamma = p.gamma || 2.2;
+        this.exposure = p.exposure || 1.0;
+        this.toneMapping = p.toneMapping || 'reinhard';
+        this.antiAliasing = p.antiAliasing || 'supersampling';
+        this.denoising = p.denoising || false;
+        this.denoiseStrength = p.denoiseStrength || 0.5;
+    }
+
+    updateBackground(type, intensity = 1.0) {                        // ray-tracer.js:568-585
+        this.world.skyIntensity = intensity;
+        this.world.backgroundKind = BG[type] !== undefined && type !== 'nan' ? BG[type] : BG.gradient;
+        this.world.solidColor = new Vec3(0.1, 0.1, 0.1);
+    }
+
+    async render(onProgress) {
+        checkSupported(this);
+        const res = await gpuRender(this, onProgress, this.opts);
+        if (!res) return;
+        blit(this, res);
+        this.lastStats = res.stats;
+        if (onProgress) onProgress(1.0);
+    }
+
+    // Everything render() computes, plus diagnostics (linear mean, per-pixel segments / draws).
+    async renderBuffers(opts = {}) {
+        return gpuRender(this, opts.onProgress, { ...this.opts, ...opts });
+    }
+}

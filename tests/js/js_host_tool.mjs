@@ -1,0 +1,89 @@
+// Test driver for the Node host (called by tests/test_js_host.py).  TEST INFRASTRUCTURE.
+//   node js_host_tool.mjs pack <case>...          -> JSON: packed desc + settings per golden case
+//   node js_host_tool.mjs render <outdir> <case>... -> GPU render of golden cases via GpuRayTracer
+//   node js_host_tool.mjs refpack <refdir> <case>... -> pack the REAL reference RayTracer's world
+import fs from 'fs';
+import path from 'path';
+import { fileURLToPath, pathToFileURL } from 'url';
+import { GpuRayTracer, settingsOf, installGpuRender } from '../../blenderraytracer_amd/js/gpu-ray-tracer.mjs';
+import { packScene } from '../../blenderraytracer_amd/js/pack.mjs';
+import { KeyedStream } from '../../blenderraytracer_amd/js/keyed-rng.mjs';
+
+const HERE = path.dirname(fileURLToPath(import.meta.url));
+const REPO = path.resolve(HERE, '..', '..');
+const manifest = JSON.parse(fs.readFileSync(path.join(REPO, 'tests', 'golden', 'manifest.json'), 'utf8'));
+const scene = (name) => JSON.parse(fs.readFileSync(path.join(REPO, 'scenes', name.endsWith('.json') ? name : name + '.json'), 'utf8'));
+const b64 = (a) => Buffer.from(a.buffer, a.byteOffset, a.byteLength).toString('base64');
+
+function tracerFor(name, extra = {}) {
+    const c = manifest.cases[name];
+    const rt = new GpuRayTracer({ width: c.requested[0], height: c.requested[1] }, { seed: c.seed, ...extra });
+    if (!rt.loadFromJSON(scene(c.scene))) throw new Error('loadFromJSON failed');
+    rt.updateRenderSettings(c.settings_in);
+    if (c.background_in) rt.updateBackground(c.background_in.type, c.background_in.intensity);
+    return { rt, c };
+}
+
+function dumpPacked(p, st) {
+    return {
+        objects: b64(p.objects), materials: b64(p.materials), triangles: b64(p.triangles), camera: Array.from(p.camera),
+        cameraType: p.cameraType, background: p.background, skyIntensity: p.skyIntensity,
+        solidColor: Array.from(p.solidColor), perm: Array.from(p.perm), settings: st,
+    };
+}
+
+async function main() {
+const [cmd, ...args] = process.argv.slice(2);
+if (cmd === 'pack') {
+    const out = {};
+    for (const name of args) {
+        const { rt, c } = tracerFor(name);
+        out[name] = dumpPacked(packScene(rt.world, rt.camera), settingsOf(rt, { seed: c.seed, crop: c.crop }));
+    }
+    process.stdout.write(JSON.stringify(out));
+} else if (cmd === 'render') {
+    const outdir = args[0];
+    const precision = process.env.RT_PRECISION || 'f64';
+    const summary = {};
+    for (const name of args.slice(1)) {
+        const { rt, c } = tracerFor(name, { precision });
+        const res = await rt.renderBuffers({ crop: c.crop, wantMean: true, wantCounts: true });
+        for (const k of ['mean', 'post', 'rgba8', 'segments', 'draws']) fs.writeFileSync(path.join(outdir, `${name}.${k}.bin`), Buffer.from(res[k].buffer));
+        summary[name] = res.stats;
+    }
+    // RayTracer.render() surface: imageData filled, onProgress ends at 1.0
+    const { rt } = tracerFor('sample_scene_aa_none');
+    const seen = [];
+    await rt.render((f) => seen.push(f));
+    summary._render = { progress: seen, nonzero: rt.imageData.data.some((v, i) => i % 4 !== 3 && v > 0) };
+    fs.writeFileSync(path.join(outdir, 'summary.json'), JSON.stringify(summary));
+} else if (cmd === 'refpack') {
+    // The drop-in: the reference's own RayTracer (temp copy prepared by the caller), its render()
+    // swapped for the GPU one; here only its packing is compared (no GPU in the build container).
+    const refdir = args[0];
+    global.window = { renderCancelled: false };
+    global.performance = { now: () => Date.now() };
+    console.log = () => {}; console.warn = () => {}; console.error = () => {};
+    const { RayTracer } = await import(pathToFileURL(path.join(refdir, 'js', 'ray-tracer.js')).href);
+    const out = {};
+    for (const name of args.slice(1)) {
+        const c = manifest.cases[name];
+        const canvas = { width: c.requested[0], height: c.requested[1], style: {}, getContext: () => ({ createImageData: (w, h) => ({ data: new Uint8ClampedArray(w * h * 4) }), putImageData() {} }) };
+        const st = new KeyedStream(c.seed);
+        Math.random = () => st.next();
+        st.select(0xFFFFFFFE, 0xFFFFFFFE);
+        const rt = new RayTracer(canvas);
+        st.select(0xFFFFFFFF, 0xFFFFFFFF);
+        rt.loadFromJSON(scene(c.scene));
+        rt.updateRenderSettings(c.settings_in);
+        if (c.background_in) rt.updateBackground(c.background_in.type, c.background_in.intensity);
+        installGpuRender(rt, { seed: c.seed });
+        out[name] = dumpPacked(packScene(rt.world, rt.camera), settingsOf(rt, { seed: c.seed, crop: c.crop }));
+    }
+    process.stdout.write(JSON.stringify(out));
+} else {
+    throw new Error('unknown command ' + cmd);
+}
+}
+
+main().catch((e) => { process.stderr.write(String(e && e.stack || e) + '\n'); process.exit(1); });

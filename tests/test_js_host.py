@@ -1,0 +1,151 @@
+"""The Node host (blenderraytracer_amd/js, rt_napi.node): packing parity with the Python host and
+with the REAL reference objects, addon loading, and (GPU) renders through the JS drop-in."""
+import base64
+import json
+import os
+import shutil
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import golden_cases as gc
+from blenderraytracer_amd.renderer import settings_struct
+from blenderraytracer_amd.scene import SCENES_DIR
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOOL = os.path.join(ROOT, "tests", "js", "js_host_tool.mjs")
+ADDON = os.path.join(ROOT, "blenderraytracer_amd", "lib", "rt_napi.node")
+NODE = shutil.which("node")
+REFERENCE = "/root/reference"
+
+pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
+
+OBJ_DT = np.dtype([("type", "<i4"), ("material", "<i4"), ("first", "<i4"), ("count", "<i4"), ("g", "<f8", 6)])
+MAT_DT = np.dtype([("type", "<i4"), ("_pad", "<i4"), ("albedo", "<f8", 3), ("roughness", "<f8"), ("ior", "<f8"),
+                   ("emission", "<f8", 3)])
+
+
+def ensure_mesh50k():
+    p = os.path.join(SCENES_DIR, "mesh50k.json")
+    if not os.path.exists(p):
+        from blenderraytracer_amd.scene import load_scene_json
+        with open(p, "w") as f:
+            json.dump(load_scene_json("mesh50k"), f)
+
+
+def run_tool(*args, env=None):
+    ensure_mesh50k()
+    out = subprocess.run([NODE, TOOL, *args], cwd=ROOT, capture_output=True, env=env, timeout=600)
+    assert out.returncode == 0, out.stderr.decode()[-3000:]
+    return out.stdout
+
+
+def canonical(objects, materials, triangles):
+    """Per-object (type, geometry, resolved material, triangles) — independent of how materials are
+    deduplicated into the table."""
+    res = []
+    for o in objects:
+        m = materials[o["material"]]
+        mat = (int(m["type"]), tuple(m["albedo"]), float(m["roughness"]), float(m["ior"]), tuple(m["emission"]))
+        tris = triangles[o["first"]:o["first"] + o["count"]].tobytes() if o["type"] in (3, 4) else b""
+        g = tuple(o["g"]) if o["type"] not in (3, 4) else ()
+        res.append((int(o["type"]), g, mat, int(o["count"]) if o["type"] in (3, 4) else 0, tris))
+    return res
+
+
+def js_canonical(d):
+    objs = np.frombuffer(base64.b64decode(d["objects"]), dtype=OBJ_DT)
+    mats = np.frombuffer(base64.b64decode(d["materials"]), dtype=MAT_DT)
+    tris = np.frombuffer(base64.b64decode(d["triangles"]), dtype="<f8").reshape(-1, 12)
+    return canonical(objs, mats, tris)
+
+
+def py_canonical(packed):
+    objs = np.frombuffer(bytes(packed.objects), dtype=OBJ_DT)[:packed.num_objects]
+    mats = np.frombuffer(bytes(packed.materials), dtype=MAT_DT)
+    return canonical(objs, mats, packed.triangles[:packed.num_triangles])
+
+
+def check_against_python(name, d):
+    rt, c = gc.tracer_for(name)
+    p = rt.packed()
+    assert js_canonical(d) == py_canonical(p), name
+    cam = p.desc.camera
+    py_cam = [*cam.origin, *cam.lower_left, *cam.horizontal, *cam.vertical, *cam.u, *cam.v, *cam.w, cam.lens_radius]
+    assert d["camera"] == py_cam, name                      # bit-identical doubles
+    assert d["cameraType"] == cam.type
+    assert d["background"] == p.desc.background
+    assert d["skyIntensity"] == p.desc.sky_intensity
+    if p.desc.background == 1:
+        assert d["solidColor"] == list(p.desc.solid_color)
+    assert d["perm"] == list(p.desc.perm)
+    st = rt.settings(crop=c["crop"])
+    js = d["settings"]
+    assert (js["width"], js["height"], js["samples"], js["maxDepth"], js["aaMode"], js["toneMap"]) == \
+        (st.width, st.height, st.samples, st.max_depth, st.aa_mode, st.tone_map), name
+    assert (js["exposure"], js["gamma"], js["seed"]) == (st.exposure, st.gamma, st.seed)
+    assert (js["cropX0"], js["cropY0"], js["cropW"], js["cropH"]) == (st.crop_x0, st.crop_y0, st.crop_w, st.crop_h)
+
+
+def test_js_packing_matches_python_host():
+    cases = gc.case_names()
+    out = json.loads(run_tool("pack", *cases))
+    for name in cases:
+        check_against_python(name, out[name])
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REFERENCE, "js")), reason="reference only in the build container")
+def test_js_packing_of_real_reference_objects():
+    """installGpuRender() on the reference's own RayTracer: the packer reads the reference's World,
+    geometry, material, Camera and background-function objects and produces the same scene."""
+    d = tempfile.mkdtemp(prefix="rt-ref-")
+    try:
+        os.makedirs(os.path.join(d, "js"))
+        for f in os.listdir(os.path.join(REFERENCE, "js")):
+            src = open(os.path.join(REFERENCE, "js", f)).read()
+            if f == "ray-tracer.js":   # optional chaining does not parse on Node 12 (off the render path)
+                import re
+                src = re.sub(r"this\.camera\?\.([A-Za-z]+)", r"(this.camera && this.camera.\1)", src)
+            open(os.path.join(d, "js", f), "w").write(src)
+        open(os.path.join(d, "package.json"), "w").write('{"type":"module"}')
+        cases = gc.case_names()
+        out = json.loads(run_tool("refpack", d, *cases))
+        for name in cases:
+            check_against_python(name, out[name])
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def test_addon_loads_without_gpu_and_fails_loudly():
+    if not os.path.exists(ADDON):
+        pytest.skip("rt_napi.node not built")
+    code = ("const m=require(%r); if (m.abiVersion()!==1) process.exit(3);"
+            "if (m.deviceCount()===0) { try { m.createScene({camera:new Float64Array(22),perm:new Int32Array(512)},0);"
+            " process.exit(4);} catch(e) { if(!/no HIP device/.test(e.message)) process.exit(5);} }") % ADDON
+    r = subprocess.run([NODE, "-e", code], capture_output=True)
+    assert r.returncode == 0, r.stderr.decode()
+
+
+@pytest.mark.gpu
+def test_js_gpu_render_matches_reference(gpu):
+    assert os.path.exists(ADDON), "rt_napi.node missing on the GPU box"
+    cases = gc.case_names()
+    with tempfile.TemporaryDirectory() as outdir:
+        run_tool("render", outdir, *cases)
+        summary = json.load(open(os.path.join(outdir, "summary.json")))
+        for name in cases:
+            c = gc.manifest()["cases"][name]
+            _, _, cw, ch = c["crop"]
+            ld = lambda k, dt: np.fromfile(os.path.join(outdir, f"{name}.{k}.bin"), dtype=dt)
+            mean = ld("mean", np.float64).reshape(ch, cw, 3)
+            lin = gc.load_array(name, "linear")
+            assert np.array_equal(ld("segments", np.uint32).reshape(ch, cw), gc.load_array(name, "segs")), name
+            assert np.array_equal(ld("draws", np.uint32).reshape(ch, cw), gc.load_array(name, "draws")), name
+            assert np.array_equal(np.isnan(mean), np.isnan(lin))
+            ok = ~np.isnan(lin)
+            assert np.all(np.abs(mean[ok] - lin[ok]) <= 1e-12 * np.maximum(1, np.abs(lin[ok]))), name
+            assert np.mean(ld("rgba8", np.uint8).reshape(ch, cw, 4) == gc.load_array(name, "rgba8")) >= 0.9999
+        r = summary["_render"]
+        assert r["progress"][-1] == 1.0 and r["nonzero"]
