@@ -115,7 +115,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(rt, cfg, args.cpu_crop)
 
-    job = ShardedRender(rt, rank=rank, world=world, device=local)
+    job = ShardedRender(rt, rank=rank, world=world, device=torch.device("cuda", local))
     for _ in range(args.warmup):
         job.step()
     torch.cuda.synchronize()

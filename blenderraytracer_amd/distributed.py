@@ -1,10 +1,11 @@
 """Multi-GPU rendering: one process per GPU, torch.distributed over RCCL (backend "nccl").
 
 Every sample is independent and keyed by (seed, pixel, sample), so rank r traces
-samples [r*S/N, (r+1)*S/N) of EVERY pixel (sample split balances better than row bands,
-where sky rows are cheap) into a float64 per-pixel sum buffer in its own HBM.  The only exchange is
-one reduce(SUM) of that buffer to rank 0 over xGMI (W*H*3 doubles: 50 MB at 1080p), after which rank
-0 runs the epilogue.  The result equals the 1-GPU render up to the order of N partial-sum additions.
+samples [r*S/N, (r+1)*S/N) of EVERY pixel (a sample split balances better than row
+bands, where sky rows are cheap) into a float64 per-pixel sum buffer in its own HBM.  The only
+exchange is one reduce(SUM) of that buffer to rank 0 over xGMI (W*H*3 doubles: 50 MB at 1080p),
+after which rank 0 runs the epilogue.  The result equals the 1-GPU render up to the order in which
+the N partial sums are added.
 """
 import ctypes as C
 
@@ -27,36 +28,50 @@ def reduce_sums(buf, world, group=None):
 
 
 class ShardedRender:
-    """One rank's share of a frame: trace own sample range -> reduce -> (rank 0) finalize on device."""
+    """One rank's share of a frame: trace own sample range -> reduce -> (rank 0) epilogue on device.
 
-    def __init__(self, tracer, rank=0, world=1, device=0, group=None):
+    trace_fn(buf, settings) may replace the HIP trace (tests run the sharding + gloo reduce on CPU
+    with the kernel's CPU build); the product path always uses rt_trace_device."""
+
+    def __init__(self, tracer, rank=0, world=1, device=None, group=None, trace_fn=None):
         self.tracer = tracer
         self.rank, self.world, self.group = rank, world, group
-        self.device = torch.device("cuda", device)
-        self.lib = capi.load_library()
-        self.scene = tracer.scene_handle()
+        self.device = device if device is not None else torch.device("cuda", 0)
+        self.stats = capi.Stats()
         s = tracer.settings()
+        self.full_settings = s
         self.n = (s.crop_w or s.width) * (s.crop_h or s.height)
         self.samples = s.samples
         self.range = sample_range(rank, world, self.samples)
         self.settings = tracer.settings(sample_range=self.range) if self.range[1] > self.range[0] else None
-        self.full_settings = s
         self.sum = torch.zeros(self.n * 3, dtype=torch.float64, device=self.device)
-        self.rgba8 = torch.zeros(self.n * 4, dtype=torch.uint8, device=self.device) if rank == 0 else None
-        self.post = torch.zeros(self.n * 4, dtype=torch.float32, device=self.device) if rank == 0 else None
-        self.stats = capi.Stats()
+        self._trace = trace_fn
+        self.rgba8 = self.post = None
+        if trace_fn is None:
+            self.lib = capi.load_library()
+            self.scene = tracer.scene_handle()
+            if rank == 0:
+                self.rgba8 = torch.zeros(self.n * 4, dtype=torch.uint8, device=self.device)
+                self.post = torch.zeros(self.n * 4, dtype=torch.float32, device=self.device)
+
+    def _hip_trace(self, stats):
+        stream = torch.cuda.current_stream(self.device)
+        capi.check(self.lib.rt_trace_device(self.scene, C.byref(self.settings), C.c_void_p(self.sum.data_ptr()),
+                                            C.c_void_p(stream.cuda_stream), 1 if stats else 0,
+                                            C.byref(self.stats) if stats else None))
 
     def step(self, stats=True):
-        """Render the frame once. With stats=True the trace kernel's HIP-event time and segment count
-        land in self.stats (the call then synchronizes the stream after the trace)."""
-        stream = torch.cuda.current_stream(self.device)
+        """Render the frame once.  With stats=True (HIP path) the trace kernel's HIP-event time and
+        segment count land in self.stats (the call then synchronizes the stream after the trace)."""
         self.sum.zero_()
         if self.settings is not None:
-            capi.check(self.lib.rt_trace_device(self.scene, C.byref(self.settings), C.c_void_p(self.sum.data_ptr()),
-                                                C.c_void_p(stream.cuda_stream), 1 if stats else 0,
-                                                C.byref(self.stats) if stats else None))
+            if self._trace is not None:
+                self._trace(self.sum, self.settings)
+            else:
+                self._hip_trace(stats)
         reduce_sums(self.sum, self.world, self.group)
-        if self.rank == 0:
+        if self.rank == 0 and self._trace is None:
+            stream = torch.cuda.current_stream(self.device)
             capi.check(self.lib.rt_finalize_device(C.byref(self.full_settings), C.c_void_p(self.sum.data_ptr()), None,
                                                    C.c_void_p(self.post.data_ptr()), C.c_void_p(self.rgba8.data_ptr()),
                                                    C.c_void_p(stream.cuda_stream)))
