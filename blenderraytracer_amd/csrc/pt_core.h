@@ -67,6 +67,9 @@ enum RunKind : int { RUN_SPHERES = 0, RUN_PLANES = 1, RUN_BOXES = 2, RUN_TRIANGL
 struct Run { int kind, begin, end, mat; };   // consecutive world objects of one kind (mat: mesh material)
 
 template <class R> struct SphereRec { R cx, cy, cz, r2; };            // r2 = radius*radius (geometry.js:19)
+// binary32 pre-filter record of a sphere (f64 mode only): centre and r^2 rounded to f32, and
+// k = 2|c|^2 + r^2 rounded up; see sphere_filter_bound below.
+struct SphereFilter { float cx, cy, cz, r2, k, pad0, pad1, pad2; };
 template <class R> struct PlaneRec { R px, py, pz, nx, ny, nz; };
 template <class R> struct BoxRec { R mnx, mny, mnz, mxx, mxy, mxz; };
 template <class R> struct TriRec { R v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z, nx, ny, nz; };  // e1=v1-v0, e2=v2-v0
@@ -78,6 +81,7 @@ struct SceneView {
     int num_runs;
     int num_prims;                 // primitives tested per segment (brute force)
     const SphereRec<R>* spheres;
+    const SphereFilter* sphere_filter;   // f64 mode: binary32 pre-filter records (same order)
     const R* sphere_r;             // radius (normal = (p - c) / r, geometry.js:34)
     const PlaneRec<R>* planes;
     const BoxRec<R>* boxes;
@@ -102,6 +106,44 @@ enum HitKind : int { HIT_NONE = -1, HIT_SPHERE = 0, HIT_PLANE = 1, HIT_BOX = 2, 
 template <class R>
 struct Closest { R t; int kind, idx, mat; };
 
+// Sphere.hit (geometry.js:15-45) folded into World.hit's strict-< acceptance, in R arithmetic.
+template <class R>
+RT_HD void sphere_test_f64(const SceneView<R>& sc, V3<R> o, V3<R> d, R a, R tmin, int i, Closest<R>& b) {
+    const SphereRec<R> s = sc.spheres[i];
+    R ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
+    R hb = ocx * d.x + ocy * d.y + ocz * d.z;
+    R c = (ocx * ocx + ocy * ocy + ocz * ocz) - s.r2;
+    R disc = hb * hb - a * c;
+    if (disc < (R)0) return;
+    R sq = sqrt(disc);
+    R root = (-hb - sq) / a;
+    if (root < tmin || b.t < root) {
+        root = (-hb + sq) / a;
+        if (root < tmin || b.t < root) return;
+    }
+    if (root < b.t) b = Closest<R>{root, HIT_SPHERE, i, sc.sphere_mat[i]};
+}
+
+// sphere_filter_bound: with exact inputs o, c, d, r (binary64 values) DISC = |d|^2 (r^2 - p^2),
+// p the line-to-centre distance.  Evaluated in binary32 from rounded inputs (u = 2^-24):
+//   |oc32 - OC|_i <= 2.0001u M_i, M_i = |o_i| + |c_i|;  |hb32 - HB| <= 6.1u S, S = sum |d_i| M_i;
+//   |cc32 - CC| <= 8.1u Q, Q = sum M_i^2 + r^2;  |a32 - A| <= 5.01u A;
+//   => |disc32 - DISC| <= 12.2u S^2 + 14.2u A Q + 2u A Q <= 28.4u A Q   (S^2 <= A sum M_i^2).
+// The binary64 evaluation is within 28.4 * 2^-53 A Q of DISC.  Q <= 2|o|^2 + 2|c|^2 + r^2, so
+// E = 2^-17 * a32 * (2|o|^2 + k), k = 2|c|^2 + r^2 (rounded up), bounds |disc32 - disc64| with a
+// 4.5x margin: disc64 >= 0 implies disc32 + E >= 0, and a filtered-out sphere is a sure miss.
+// tests/test_sphere_filter.py checks the bound on adversarial random cases.
+
+// false only if the sphere is certainly missed in binary64 (disc64 < 0); NaN never rejects.
+RT_HD bool sphere_filter_pass(const SphereFilter& f, float ox, float oy, float oz, float dx, float dy, float dz,
+                              float a32, float beta, float alpha) {
+    const float ocx = ox - f.cx, ocy = oy - f.cy, ocz = oz - f.cz;
+    const float hb = __builtin_fmaf(ocx, dx, __builtin_fmaf(ocy, dy, ocz * dz));
+    const float cc = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz)) - f.r2;
+    const float disc = __builtin_fmaf(hb, hb, -(a32 * cc));
+    return !(disc + __builtin_fmaf(beta, f.k, alpha) < 0.0f);
+}
+
 // Closest hit over the whole world: World.hit (world.js:20-33) with every object's hit() inlined.
 // All lanes walk the same primitive list in the same order, so every record load — including the
 // material index, taken at accept time — is wave-uniform (scalar loads, no LDS).  Only
@@ -115,24 +157,24 @@ RT_HD Closest<R> closest_hit(const SceneView<R>& sc, V3<R> o, V3<R> d) {
     for (int r = 0; r < sc.num_runs; ++r) {
         const Run run = sc.runs[r];
         if (run.kind == RUN_SPHERES) {
-#pragma unroll 2
-            for (int i = run.begin; i < run.end; ++i) {                       // geometry.js:15-45
-                const SphereRec<R> s = sc.spheres[i];
-                R ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
-                R hb = ocx * d.x + ocy * d.y + ocz * d.z;
-                R c = (ocx * ocx + ocy * ocy + ocz * ocz) - s.r2;
-                R disc = hb * hb - a * c;
-                if (!(disc < (R)0)) {
-                    R sq = sqrt(disc);
-                    R root = (-hb - sq) / a;
-                    bool ok = true;
-                    if (root < tmin || b.t < root) {
-                        root = (-hb + sq) / a;
-                        ok = !(root < tmin || b.t < root);
-                    }
-                    if (ok && root < b.t) b = Closest<R>{root, HIT_SPHERE, i, sc.sphere_mat[i]};
+            if constexpr (sizeof(R) == 8) {
+                // Exact mode: every sphere is first tested in binary32 with a rigorous bound E on
+                // |disc32 - disc64| (sphere_filter_bound); only spheres the filter cannot reject get
+                // the binary64 test below, so every decision is the f64 one, at ~f32 cost per miss.
+                const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+                const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+                const float a32 = dx * dx + dy * dy + dz * dz;
+                const float beta = a32 * 0x1p-17f;                             // E = beta*k + alpha
+                const float alpha = beta * (2.0f * (ox * ox + oy * oy + oz * oz));
+#pragma unroll 4
+                for (int i = run.begin; i < run.end; ++i) {
+                    if (!sphere_filter_pass(sc.sphere_filter[i], ox, oy, oz, dx, dy, dz, a32, beta, alpha)) continue;
+                    sphere_test_f64(sc, o, d, a, tmin, i, b);
                 }
+                continue;
             }
+#pragma unroll 2
+            for (int i = run.begin; i < run.end; ++i) sphere_test_f64(sc, o, d, a, tmin, i, b);
         } else if (run.kind == RUN_PLANES) {
             for (int i = run.begin; i < run.end; ++i) {                       // geometry.js:56-74
                 const PlaneRec<R> p = sc.planes[i];

@@ -103,6 +103,7 @@ inline bool pack_host(const rt_scene_desc& d, HostScene& hs, std::string& err) {
 template <class R>
 struct HostRecords {
     std::vector<SphereRec<R>> spheres;
+    std::vector<SphereFilter> sphere_filter;
     std::vector<R> sphere_r;
     std::vector<PlaneRec<R>> planes;
     std::vector<BoxRec<R>> boxes;
@@ -121,6 +122,13 @@ void make_records(const HostScene& hs, const rt_scene_desc& d, HostRecords<R>& o
         out.spheres[i] = SphereRec<R>{(R)s[0], (R)s[1], (R)s[2], sizeof(R) == 8 ? (R)s[3] : r * r};
     }
     out.sphere_r.assign(hs.sphere_r.begin(), hs.sphere_r.end());
+    out.sphere_filter.resize(hs.sphere_r.size());
+    for (size_t i = 0; i < out.sphere_filter.size(); ++i) {
+        const double* s = &hs.spheres[4 * i];
+        const double k = 2.0 * (s[0] * s[0] + s[1] * s[1] + s[2] * s[2]) + s[3];
+        out.sphere_filter[i] = SphereFilter{(float)s[0], (float)s[1], (float)s[2], (float)s[3],
+                                            (float)(k * (1.0 + 0x1p-20)), 0.f, 0.f, 0.f};   // k rounded up
+    }
     out.planes.resize(hs.plane_mat.size());
     for (size_t i = 0; i < out.planes.size(); ++i) {
         const double* p = &hs.planes[6 * i];

@@ -18,7 +18,7 @@ static int render(const rt_scene_desc* d, const rt_settings* s, double* sum, uin
     make_records(hs, *d, rec);
     SceneView<R> v{};
     v.runs = hs.runs.data();
-    v.spheres = rec.spheres.data(); v.sphere_r = rec.sphere_r.data(); v.planes = rec.planes.data();
+    v.spheres = rec.spheres.data(); v.sphere_filter = rec.sphere_filter.data(); v.sphere_r = rec.sphere_r.data(); v.planes = rec.planes.data();
     v.boxes = rec.boxes.data(); v.tris = rec.tris.data(); v.sphere_mat = hs.sphere_mat.data();
     v.plane_mat = hs.plane_mat.data(); v.box_mat = hs.box_mat.data(); v.tri_mat = hs.tri_mat.data();
     v.mats = rec.mats.data(); v.perm = rec.perm.data();
@@ -47,4 +47,64 @@ static int render(const rt_scene_desc* d, const rt_settings* s, double* sum, uin
 
 extern "C" int ptc_render(const rt_scene_desc* d, const rt_settings* s, double* sum, uint32_t* segs, uint32_t* draws) {
     return s->precision == RT_PREC_F32 ? render<float>(d, s, sum, segs, draws) : render<double>(d, s, sum, segs, draws);
+}
+
+// Adversarial check of the binary32 sphere pre-filter (pt_core.h sphere_filter_pass): random spheres
+// over 7 decades of scale, rays aimed at |p| = r (1 +- eps) from the centre so disc64 sits at 0.
+// Returns the number of spheres the filter rejected although disc64 >= 0 (must be 0); writes the
+// largest |disc32 - disc64| / (A Q) seen and the fraction of sure misses the filter rejects.
+#include <cmath>
+#include <random>
+extern "C" int ptc_sphere_filter_check(long long n, unsigned seed, double* max_ratio, double* reject_frac) {
+    std::mt19937_64 gen(seed);
+    std::uniform_real_distribution<double> U(-1.0, 1.0);
+    long long violations = 0, misses = 0, rejected = 0;
+    double worst = 0;
+    for (long long it = 0; it < n; ++it) {
+        const double scale = std::pow(10.0, 4.0 * U(gen) + 0.5);      // scene scale 10^-3.5 .. 10^4.5
+        const double r = std::fabs(U(gen)) * scale * 0.5 + 1e-9;
+        const double c[3] = {U(gen) * scale, U(gen) * scale, U(gen) * scale};
+        double dd[3] = {U(gen), U(gen), U(gen)};
+        const double dl = std::pow(10.0, 3.0 * U(gen));                // |d| 10^-3 .. 10^3 (unnormalized)
+        // a point at distance r*(1+eps) from the centre, perpendicular to d, then back off along d
+        double w[3] = {U(gen), U(gen), U(gen)};
+        const double wd = (w[0] * dd[0] + w[1] * dd[1] + w[2] * dd[2]) / (dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]);
+        for (int k = 0; k < 3; ++k) w[k] -= wd * dd[k];
+        const double wn = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+        const double eps = (it & 1 ? 1 : -1) * std::pow(10.0, -7.0 * std::fabs(U(gen)) - 1.0);
+        const double back = U(gen) * 4 * scale;
+        double o[3], d[3];
+        for (int k = 0; k < 3; ++k) {
+            d[k] = dd[k] * dl;
+            o[k] = c[k] + w[k] / wn * r * (1 + eps) - dd[k] * back;
+        }
+        const double ocx = o[0] - c[0], ocy = o[1] - c[1], ocz = o[2] - c[2];
+        const double a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+        const double hb = ocx * d[0] + ocy * d[1] + ocz * d[2];
+        const double cc = (ocx * ocx + ocy * ocy + ocz * ocz) - r * r;
+        const double disc64 = hb * hb - a * cc;
+        const double k = 2.0 * (c[0] * c[0] + c[1] * c[1] + c[2] * c[2]) + r * r;
+        SphereFilter f{(float)c[0], (float)c[1], (float)c[2], (float)(r * r), (float)(k * (1.0 + 0x1p-20)), 0, 0, 0};
+        const float ox = (float)o[0], oy = (float)o[1], oz = (float)o[2];
+        const float dx = (float)d[0], dy = (float)d[1], dz = (float)d[2];
+        const float a32 = dx * dx + dy * dy + dz * dz;
+        const float beta = a32 * 0x1p-17f;
+        const float alpha = beta * (2.0f * (ox * ox + oy * oy + oz * oz));
+        const bool pass = sphere_filter_pass(f, ox, oy, oz, dx, dy, dz, a32, beta, alpha);
+        if (disc64 >= 0 && !pass) ++violations;
+        if (disc64 < 0) { ++misses; rejected += !pass; }
+        // observed error of the binary32 discriminant against the binary64 one
+        const float focx = ox - f.cx, focy = oy - f.cy, focz = oz - f.cz;
+        const float fhb = __builtin_fmaf(focx, dx, __builtin_fmaf(focy, dy, focz * dz));
+        const float fcc = __builtin_fmaf(focx, focx, __builtin_fmaf(focy, focy, focz * focz)) - f.r2;
+        const float fdisc = __builtin_fmaf(fhb, fhb, -(a32 * fcc));
+        double Q = 0;
+        for (int q = 0; q < 3; ++q) Q += (std::fabs(o[q]) + std::fabs(c[q])) * (std::fabs(o[q]) + std::fabs(c[q]));
+        Q += r * r;
+        const double ratio = std::fabs((double)fdisc - disc64) / (a * Q);
+        if (ratio > worst) worst = ratio;
+    }
+    *max_ratio = worst;
+    *reject_frac = misses ? (double)rejected / misses : 0;
+    return (int)violations;
 }
