@@ -67,9 +67,9 @@ enum RunKind : int { RUN_SPHERES = 0, RUN_PLANES = 1, RUN_BOXES = 2, RUN_TRIANGL
 struct Run { int kind, begin, end, mat; };   // consecutive world objects of one kind (mat: mesh material)
 
 template <class R> struct SphereRec { R cx, cy, cz, r2; };            // r2 = radius*radius (geometry.js:19)
-// binary32 pre-filter record of a sphere (f64 mode only): centre and r^2 rounded to f32, and
-// k = 2|c|^2 + r^2 rounded up; see sphere_filter_bound below.
-struct SphereFilter { float cx, cy, cz, r2, k, pad0, pad1, pad2; };
+// binary32 pre-filter record of a sphere (f64 mode only): centre rounded to f32 and the radius^2
+// inflated by the error bound, r2p = r^2 + 2^-17 (2|c|^2 + r^2), rounded up; see sphere_filter_bound.
+struct SphereFilter { float cx, cy, cz, r2p; };
 template <class R> struct PlaneRec { R px, py, pz, nx, ny, nz; };
 template <class R> struct BoxRec { R mnx, mny, mnz, mxx, mxy, mxz; };
 template <class R> struct TriRec { R v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z, nx, ny, nz; };  // e1=v1-v0, e2=v2-v0
@@ -82,6 +82,7 @@ struct SceneView {
     int num_prims;                 // primitives tested per segment (brute force)
     const SphereRec<R>* spheres;
     const SphereFilter* sphere_filter;   // f64 mode: binary32 pre-filter records (same order)
+    int num_spheres;
     const R* sphere_r;             // radius (normal = (p - c) / r, geometry.js:34)
     const PlaneRec<R>* planes;
     const BoxRec<R>* boxes;
@@ -106,6 +107,16 @@ enum HitKind : int { HIT_NONE = -1, HIT_SPHERE = 0, HIT_PLANE = 1, HIT_BOX = 2, 
 template <class R>
 struct Closest { R t; int kind, idx, mat; };
 
+// Filter records staged in LDS by the workgroup (pt_trace.hip), read by every lane at the same
+// address (broadcast ds_read_b128).
+struct LdsSpheres { const SphereFilter* rec; };
+
+#ifndef RT_SPHERE_UNROLL
+#define RT_SPHERE_UNROLL 16
+#endif
+#define RT_PRAGMA(x) _Pragma(#x)
+#define RT_UNROLL(n) RT_PRAGMA(unroll n)
+
 // Sphere.hit (geometry.js:15-45) folded into World.hit's strict-< acceptance, in R arithmetic.
 template <class R>
 RT_HD void sphere_test_f64(const SceneView<R>& sc, V3<R> o, V3<R> d, R a, R tmin, int i, Closest<R>& b) {
@@ -124,24 +135,35 @@ RT_HD void sphere_test_f64(const SceneView<R>& sc, V3<R> o, V3<R> d, R a, R tmin
     if (root < b.t) b = Closest<R>{root, HIT_SPHERE, i, sc.sphere_mat[i]};
 }
 
-// sphere_filter_bound: with exact inputs o, c, d, r (binary64 values) DISC = |d|^2 (r^2 - p^2),
-// p the line-to-centre distance.  Evaluated in binary32 from rounded inputs (u = 2^-24):
-//   |oc32 - OC|_i <= 2.0001u M_i, M_i = |o_i| + |c_i|;  |hb32 - HB| <= 6.1u S, S = sum |d_i| M_i;
-//   |cc32 - CC| <= 8.1u Q, Q = sum M_i^2 + r^2;  |a32 - A| <= 5.01u A;
-//   => |disc32 - DISC| <= 12.2u S^2 + 14.2u A Q + 2u A Q <= 28.4u A Q   (S^2 <= A sum M_i^2).
-// The binary64 evaluation is within 28.4 * 2^-53 A Q of DISC.  Q <= 2|o|^2 + 2|c|^2 + r^2, so
-// E = 2^-17 * a32 * (2|o|^2 + k), k = 2|c|^2 + r^2 (rounded up), bounds |disc32 - disc64| with a
-// 4.5x margin: disc64 >= 0 implies disc32 + E >= 0, and a filtered-out sphere is a sure miss.
-// tests/test_sphere_filter.py checks the bound on adversarial random cases.
+// sphere_filter_bound.  With the exact binary64 inputs o, c, d, r: DISC = |d|^2 (r^2 - p^2), p the
+// line-to-centre distance, so the sign of Y = r^2 - p^2 = r^2 - |OC|^2 + (OC.n)^2 (n = d/|d|) decides.
+// The filter evaluates X = (oc32.dn)^2 - |oc32|^2 + r2p + delta in binary32 (u = 2^-24) from rounded
+// o, c and the normalized rounded direction dn, with r2p = r^2 + 2^-17 (2|c|^2 + r^2) and
+// delta = 2^-16 |o|^2 (both rounded up).  With M_i = |o_i| + |c_i| and Q = sum M_i^2 + r^2 <=
+// 2|o|^2 + 2|c|^2 + r^2, the rounding terms are |(oc32.dn)^2 - (OC.n)^2| <= 18u Q (oc error 2u M,
+// direction error 4u, dot 3u), ||oc32|^2 - |OC|^2| <= 7u Q and <= 2u Q for the final roundings:
+// |X - Y - (r2p - r^2) - delta| <= 27u Q, while r2p - r^2 + delta >= 2^-17 Q = 128u Q.  Hence
+// disc64 >= 0 (Y >= -2^-48 Q) implies X > 0: a rejected sphere (X < 0) is a sure binary64 miss.
+// NaN never rejects.  tests/test_sphere_filter.py checks this on adversarial near-tangent cases.
+struct FilterRay { float ox, oy, oz, dx, dy, dz, delta; };
 
-// false only if the sphere is certainly missed in binary64 (disc64 < 0); NaN never rejects.
-RT_HD bool sphere_filter_pass(const SphereFilter& f, float ox, float oy, float oz, float dx, float dy, float dz,
-                              float a32, float beta, float alpha) {
-    const float ocx = ox - f.cx, ocy = oy - f.cy, ocz = oz - f.cz;
-    const float hb = __builtin_fmaf(ocx, dx, __builtin_fmaf(ocy, dy, ocz * dz));
-    const float cc = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, ocz * ocz)) - f.r2;
-    const float disc = __builtin_fmaf(hb, hb, -(a32 * cc));
-    return !(disc + __builtin_fmaf(beta, f.k, alpha) < 0.0f);
+template <class R>
+RT_HD FilterRay make_filter_ray(V3<R> o, V3<R> d) {
+    FilterRay f;
+    f.ox = (float)o.x; f.oy = (float)o.y; f.oz = (float)o.z;
+    const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+    const float inv = 1.0f / sqrtf(dx * dx + dy * dy + dz * dz);
+    f.dx = dx * inv; f.dy = dy * inv; f.dz = dz * inv;
+    f.delta = (f.ox * f.ox + f.oy * f.oy + f.oz * f.oz) * (0x1p-16f * (1.0f + 0x1p-20f));
+    return f;
+}
+
+// false only if the sphere is certainly missed in binary64 (disc64 < 0): 12 VALU per sphere
+RT_HD bool sphere_filter_pass(const SphereFilter& s, const FilterRay& r) {
+    const float ocx = r.ox - s.cx, ocy = r.oy - s.cy, ocz = r.oz - s.cz;
+    const float hb = __builtin_fmaf(ocx, r.dx, __builtin_fmaf(ocy, r.dy, ocz * r.dz));
+    const float cc = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, __builtin_fmaf(ocz, ocz, -(s.r2p + r.delta))));
+    return !(__builtin_fmaf(hb, hb, -cc) < 0.0f);
 }
 
 // Closest hit over the whole world: World.hit (world.js:20-33) with every object's hit() inlined.
@@ -149,8 +171,8 @@ RT_HD bool sphere_filter_pass(const SphereFilter& f, float ox, float oy, float o
 // material index, taken at accept time — is wave-uniform (scalar loads, no LDS).  Only
 // (t, kind, index, material) is tracked; the hit record is rebuilt afterwards from (t, primitive),
 // which is exact because no primitive's chosen t depends on tMax.
-template <class R>
-RT_HD Closest<R> closest_hit(const SceneView<R>& sc, V3<R> o, V3<R> d) {
+template <class R, bool LDS = false>
+RT_HD Closest<R> closest_hit(const SceneView<R>& sc, V3<R> o, V3<R> d, const LdsSpheres lds = LdsSpheres{nullptr}) {
     const R tmin = (R)0.001;
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0};
     const R a = dot(d, d);
@@ -161,15 +183,19 @@ RT_HD Closest<R> closest_hit(const SceneView<R>& sc, V3<R> o, V3<R> d) {
                 // Exact mode: every sphere is first tested in binary32 with a rigorous bound E on
                 // |disc32 - disc64| (sphere_filter_bound); only spheres the filter cannot reject get
                 // the binary64 test below, so every decision is the f64 one, at ~f32 cost per miss.
-                const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
-                const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
-                const float a32 = dx * dx + dy * dy + dz * dz;
-                const float beta = a32 * 0x1p-17f;                             // E = beta*k + alpha
-                const float alpha = beta * (2.0f * (ox * ox + oy * oy + oz * oz));
-#pragma unroll 4
-                for (int i = run.begin; i < run.end; ++i) {
-                    if (!sphere_filter_pass(sc.sphere_filter[i], ox, oy, oz, dx, dy, dz, a32, beta, alpha)) continue;
-                    sphere_test_f64(sc, o, d, a, tmin, i, b);
+                const FilterRay fr = make_filter_ray(o, d);
+                if constexpr (LDS) {
+RT_UNROLL(RT_SPHERE_UNROLL)
+                    for (int i = run.begin; i < run.end; ++i) {
+                        if (!sphere_filter_pass(lds.rec[i], fr)) continue;
+                        sphere_test_f64(sc, o, d, a, tmin, i, b);
+                    }
+                } else {
+RT_UNROLL(RT_SPHERE_UNROLL)
+                    for (int i = run.begin; i < run.end; ++i) {
+                        if (!sphere_filter_pass(sc.sphere_filter[i], fr)) continue;
+                        sphere_test_f64(sc, o, d, a, tmin, i, b);
+                    }
                 }
                 continue;
             }

@@ -97,8 +97,9 @@ RT_HD bool scatter(const MatRec<R>& m, const Hit<R>& h, V3<R> d, Rng<R>& g, V3<R
 struct PixelResult { uint32_t segments, draws; };
 
 // Trace samples [im.s_begin, s_end) of crop pixel (cx, cy), adding radiance into sum[0..2].
-template <class R, bool COUNT>
-RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int cx, int cy, int s_end, double* sum) {
+template <class R, bool COUNT, bool LDS = false>
+RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int cx, int cy, int s_end, double* sum,
+                              const LdsSpheres lds = LdsSpheres{nullptr}) {
     const int i = im.x0 + cx, row = im.y0 + cy, j = im.height - 1 - row;
     const uint32_t pkey = pixel_key(im.seedm, (uint32_t)row * (uint32_t)im.width + (uint32_t)i);
     PixelResult res{0, 0};
@@ -109,7 +110,7 @@ RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int
     int depth = im.max_depth;
     if (s < s_end) start_sample(sc, im, i, j, pkey, s, g, o, d);
     while (s < s_end) {
-        const Closest<R> c = closest_hit(sc, o, d);
+        const Closest<R> c = closest_hit<R, LDS>(sc, o, d, lds);
         ++res.segments;
         bool done = true;
         V3<R> L = mk<R>(0, 0, 0);

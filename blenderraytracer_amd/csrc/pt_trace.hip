@@ -5,6 +5,8 @@
 // block, so neighbouring rays share a wave.  Primitive records are walked in World.objects order by
 // every lane in lockstep, so all record loads are wave-uniform scalar loads; the per-pixel sums are
 // read and written once per launch.
+#include <cstdlib>
+
 #include "pt_launch.h"
 
 namespace rt {
@@ -16,9 +18,21 @@ struct TraceArgs {
     Counters c;
 };
 
-template <class R, bool COUNT>
-__global__ __launch_bounds__(256) void trace_kernel(const TraceArgs<R> args) {
+#ifndef RT_MIN_WAVES_PER_SIMD
+#define RT_MIN_WAVES_PER_SIMD 8   // 64 VGPRs: latency-bound loop, 8 waves/SIMD measured fastest
+#endif
+
+template <class R, bool COUNT, bool LDS>
+__global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void trace_kernel(const TraceArgs<R> args) {
     const ImageParams& im = args.im;
+    LdsSpheres lds{nullptr};
+    if constexpr (LDS) {
+        // stage the binary32 sphere filter records of the whole scene in LDS (one copy per workgroup)
+        extern __shared__ SphereFilter lds_spheres[];
+        for (int t = threadIdx.x; t < args.sc.num_spheres; t += blockDim.x) lds_spheres[t] = args.sc.sphere_filter[t];
+        __syncthreads();
+        lds = LdsSpheres{lds_spheres};
+    }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int tiles_x = (im.cw + 15) >> 4;
     const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
@@ -29,7 +43,7 @@ __global__ __launch_bounds__(256) void trace_kernel(const TraceArgs<R> args) {
     double acc[3] = {0, 0, 0};
     if (valid) { acc[0] = args.c.sum[3 * q]; acc[1] = args.c.sum[3 * q + 1]; acc[2] = args.c.sum[3 * q + 2]; }
     // invalid lanes trace nothing but stay for the wave reduction below
-    const PixelResult r = trace_pixel<R, COUNT>(args.sc, im, cx, cy, valid ? im.s_end : im.s_begin, acc);
+    const PixelResult r = trace_pixel<R, COUNT, LDS>(args.sc, im, cx, cy, valid ? im.s_end : im.s_begin, acc, lds);
     if (valid) {
         args.c.sum[3 * q] = acc[0]; args.c.sum[3 * q + 1] = acc[1]; args.c.sum[3 * q + 2] = acc[2];
         if (COUNT) {
@@ -44,15 +58,37 @@ __global__ __launch_bounds__(256) void trace_kernel(const TraceArgs<R> args) {
     }
 }
 
+// RT_SPHERE_PATH=lds stages the 16-B sphere filter records in LDS per workgroup instead of reading them
+// with scalar loads (measured equal on RTOW); default: scalar loads.
+static int sphere_path_override() {
+    static int v = -2;
+    if (v == -2) {
+        const char* e = getenv("RT_SPHERE_PATH");
+        v = !e ? -1 : (e[0] == 'l' ? 1 : 0);
+    }
+    return v;
+}
+
 template <class R>
 hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, hipStream_t stream) {
     if (im.cw <= 0 || im.ch <= 0 || im.s_end <= im.s_begin) return hipSuccess;
     const int tiles = ((im.cw + 15) >> 4) * ((im.ch + 15) >> 4);
     TraceArgs<R> a{sc, im, c};
-    if (c.segs || c.draws)
-        hipLaunchKernelGGL((trace_kernel<R, true>), dim3(tiles), dim3(256), 0, stream, a);
-    else
-        hipLaunchKernelGGL((trace_kernel<R, false>), dim3(tiles), dim3(256), 0, stream, a);
+    const size_t lds_bytes = (size_t)sc.num_spheres * sizeof(SphereFilter);
+    const int ov = sphere_path_override();
+    const bool lds = sizeof(R) == 8 && sc.num_spheres > 0 && lds_bytes <= 48 * 1024 && ov == 1;
+    const bool count = c.segs || c.draws;
+    if constexpr (sizeof(R) == 8) {
+        if (lds) {
+            if (count) hipLaunchKernelGGL((trace_kernel<R, true, true>), dim3(tiles), dim3(256), lds_bytes, stream, a);
+            else hipLaunchKernelGGL((trace_kernel<R, false, true>), dim3(tiles), dim3(256), lds_bytes, stream, a);
+            return hipGetLastError();
+        }
+    }
+    {
+        if (count) hipLaunchKernelGGL((trace_kernel<R, true, false>), dim3(tiles), dim3(256), 0, stream, a);
+        else hipLaunchKernelGGL((trace_kernel<R, false, false>), dim3(tiles), dim3(256), 0, stream, a);
+    }
     return hipGetLastError();
 }
 

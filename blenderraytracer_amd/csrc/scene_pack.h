@@ -126,8 +126,8 @@ void make_records(const HostScene& hs, const rt_scene_desc& d, HostRecords<R>& o
     for (size_t i = 0; i < out.sphere_filter.size(); ++i) {
         const double* s = &hs.spheres[4 * i];
         const double k = 2.0 * (s[0] * s[0] + s[1] * s[1] + s[2] * s[2]) + s[3];
-        out.sphere_filter[i] = SphereFilter{(float)s[0], (float)s[1], (float)s[2], (float)s[3],
-                                            (float)(k * (1.0 + 0x1p-20)), 0.f, 0.f, 0.f};   // k rounded up
+        // r2p = r^2 + 2^-17 k, rounded up (sphere_filter_bound in pt_core.h)
+        out.sphere_filter[i] = SphereFilter{(float)s[0], (float)s[1], (float)s[2], (float)((s[3] + 0x1p-17 * k) * (1.0 + 0x1p-20))};
     }
     out.planes.resize(hs.plane_mat.size());
     for (size_t i = 0; i < out.planes.size(); ++i) {
@@ -165,6 +165,7 @@ void make_records(const HostScene& hs, const rt_scene_desc& d, HostRecords<R>& o
 template <class R>
 void fill_view_constants(SceneView<R>& v, const HostScene& hs, const rt_scene_desc& d) {
     v.num_runs = (int)hs.runs.size();
+    v.num_spheres = (int)hs.sphere_r.size();
     v.num_prims = hs.num_prims;
     const rt_camera_desc& c = d.camera;
     for (int k = 0; k < 3; ++k) {

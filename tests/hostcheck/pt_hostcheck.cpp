@@ -84,24 +84,21 @@ extern "C" int ptc_sphere_filter_check(long long n, unsigned seed, double* max_r
         const double cc = (ocx * ocx + ocy * ocy + ocz * ocz) - r * r;
         const double disc64 = hb * hb - a * cc;
         const double k = 2.0 * (c[0] * c[0] + c[1] * c[1] + c[2] * c[2]) + r * r;
-        SphereFilter f{(float)c[0], (float)c[1], (float)c[2], (float)(r * r), (float)(k * (1.0 + 0x1p-20)), 0, 0, 0};
-        const float ox = (float)o[0], oy = (float)o[1], oz = (float)o[2];
-        const float dx = (float)d[0], dy = (float)d[1], dz = (float)d[2];
-        const float a32 = dx * dx + dy * dy + dz * dz;
-        const float beta = a32 * 0x1p-17f;
-        const float alpha = beta * (2.0f * (ox * ox + oy * oy + oz * oz));
-        const bool pass = sphere_filter_pass(f, ox, oy, oz, dx, dy, dz, a32, beta, alpha);
+        SphereFilter f{(float)c[0], (float)c[1], (float)c[2], (float)((r * r + 0x1p-17 * k) * (1.0 + 0x1p-20))};
+        const FilterRay fr = make_filter_ray(V3<double>{o[0], o[1], o[2]}, V3<double>{d[0], d[1], d[2]});
+        const bool pass = sphere_filter_pass(f, fr);
         if (disc64 >= 0 && !pass) ++violations;
         if (disc64 < 0) { ++misses; rejected += !pass; }
-        // observed error of the binary32 discriminant against the binary64 one
-        const float focx = ox - f.cx, focy = oy - f.cy, focz = oz - f.cz;
-        const float fhb = __builtin_fmaf(focx, dx, __builtin_fmaf(focy, dy, focz * dz));
-        const float fcc = __builtin_fmaf(focx, focx, __builtin_fmaf(focy, focy, focz * focz)) - f.r2;
-        const float fdisc = __builtin_fmaf(fhb, fhb, -(a32 * fcc));
+        // observed |X - Y - margin| / Q of the binary32 evaluation (X, Y as in sphere_filter_bound)
+        const float fx = fr.ox - (float)c[0], fy = fr.oy - (float)c[1], fz = fr.oz - (float)c[2];
+        const float fhb = __builtin_fmaf(fx, fr.dx, __builtin_fmaf(fy, fr.dy, fz * fr.dz));
+        const float fcc = __builtin_fmaf(fx, fx, __builtin_fmaf(fy, fy, __builtin_fmaf(fz, fz, -(float)(r * r))));
+        const double X = (double)__builtin_fmaf(fhb, fhb, -fcc);
+        const double Y = disc64 / a;
         double Q = 0;
         for (int q = 0; q < 3; ++q) Q += (std::fabs(o[q]) + std::fabs(c[q])) * (std::fabs(o[q]) + std::fabs(c[q]));
         Q += r * r;
-        const double ratio = std::fabs((double)fdisc - disc64) / (a * Q);
+        const double ratio = std::fabs(X - Y) / Q;
         if (ratio > worst) worst = ratio;
     }
     *max_ratio = worst;
