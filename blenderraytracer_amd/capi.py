@@ -53,7 +53,8 @@ class Settings(C.Structure):
                 ("aa_mode", C.c_int32), ("tone_map", C.c_int32), ("exposure", C.c_double), ("gamma", C.c_double),
                 ("seed", C.c_uint32), ("sample_begin", C.c_int32), ("sample_end", C.c_int32),
                 ("crop_x0", C.c_int32), ("crop_y0", C.c_int32), ("crop_w", C.c_int32), ("crop_h", C.c_int32),
-                ("precision", C.c_int32), ("batch_samples", C.c_int32), ("_pad", C.c_int32)]
+                ("precision", C.c_int32), ("batch_samples", C.c_int32), ("denoise", C.c_int32),
+                ("denoise_weights", C.c_double * 2)]
 
 
 class Output(C.Structure):
@@ -80,8 +81,8 @@ EXPORTS = {
                             C.POINTER(Stats)]),
     "rt_trace_device": (C.c_int, [C.c_void_p, C.POINTER(Settings), C.c_void_p, C.c_void_p, C.c_int,
                                   C.POINTER(Stats)]),
-    "rt_finalize_device": (C.c_int, [C.POINTER(Settings), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                     C.c_void_p]),
+    "rt_finalize_device": (C.c_int, [C.c_void_p, C.POINTER(Settings), C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p]),
     "rt_cancel": (C.c_int, [C.c_void_p]),
 }
 

@@ -295,6 +295,9 @@ napi_value render(napi_env env, napi_callback_info info) {
     st.crop_h = (int32_t)get_num(env, s, "cropH", 0);
     st.precision = (int32_t)get_num(env, s, "precision", RT_PREC_F64);
     st.batch_samples = (int32_t)get_num(env, s, "batchSamples", 0);
+    st.denoise = (int32_t)get_num(env, s, "denoise", 0);
+    st.denoise_weights[0] = get_num(env, s, "denoiseW1", 0.0);
+    st.denoise_weights[1] = get_num(env, s, "denoiseW2", 0.0);
     job->want_mean = get_num(env, s, "wantMean", 0) != 0;
     job->want_counts = get_num(env, s, "wantCounts", 0) != 0;
     const int cw = st.crop_w > 0 ? st.crop_w : st.width, ch = st.crop_h > 0 ? st.crop_h : st.height;

@@ -25,5 +25,7 @@ struct FinalizeParams {
 };
 hipError_t launch_finalize(const FinalizeParams& p, const double* sum, double* mean, float* post, uint8_t* rgba8,
                            hipStream_t stream);
+hipError_t launch_denoise(int w, int h, double w1, double w2, const float* in, float* out, uint8_t* rgba8,
+                          hipStream_t stream);
 
 }  // namespace rt

@@ -131,4 +131,41 @@ hipError_t launch_finalize(const FinalizeParams& p, const double* sum, double* m
     return hipGetLastError();
 }
 
+// ---- PostProcessor.denoise (post-processor.js:45-77) + the RGBA8 pass of ray-tracer.js:269-275 ----
+// 3x3 Gaussian over the Float32 post-gamma frame with clamp-to-edge; accumulation in binary64 in the
+// reference's order (ky outer, kx inner); result stored as Float32, RGBA8 made from that Float32.
+__global__ __launch_bounds__(256) void denoise_kernel(const int w, const int h, const double w1, const double w2,
+                                                      const float* __restrict__ in, float* __restrict__ out,
+                                                      uint8_t* __restrict__ rgba8) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= w * h) return;
+    const int y = q / w, x = q - y * w;
+    double r = 0, g = 0, b = 0, weight = 0;
+    for (int ky = -1; ky <= 1; ++ky) {
+        for (int kx = -1; kx <= 1; ++kx) {
+            const int nx = max(0, min(w - 1, x + kx)), ny = max(0, min(h - 1, y + ky));
+            const float4 v = *reinterpret_cast<const float4*>(in + 4 * ((size_t)ny * w + nx));
+            const int d2 = kx * kx + ky * ky;
+            const double wt = d2 == 0 ? 1.0 : (d2 == 1 ? w1 : w2);
+            r += (double)v.x * wt;
+            g += (double)v.y * wt;
+            b += (double)v.z * wt;
+            weight += wt;
+        }
+    }
+    const float a = in[4 * (size_t)q + 3];
+    const float4 o = make_float4((float)(r / weight), (float)(g / weight), (float)(b / weight), a);
+    if (out) *reinterpret_cast<float4*>(out + 4 * (size_t)q) = o;
+    if (rgba8) *reinterpret_cast<uchar4*>(rgba8 + 4 * (size_t)q) =
+        make_uchar4(to_u8((double)o.x), to_u8((double)o.y), to_u8((double)o.z), 255);
+}
+
+hipError_t launch_denoise(int w, int h, double w1, double w2, const float* in, float* out, uint8_t* rgba8,
+                          hipStream_t stream) {
+    const int n = w * h;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(denoise_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, w, h, w1, w2, in, out, rgba8);
+    return hipGetLastError();
+}
+
 }  // namespace rt

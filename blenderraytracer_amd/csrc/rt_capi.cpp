@@ -126,7 +126,7 @@ struct rt_scene {
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {};
     DevBuf<double> sum, mean;
-    DevBuf<float> post;
+    DevBuf<float> post, post_raw;   // post_raw: pre-denoise floatData
     DevBuf<uint8_t> rgba;
     DevBuf<uint32_t> segs, draws;
     DevBuf<unsigned long long> total;
@@ -147,7 +147,20 @@ int check_settings(const rt_settings* s, int* cw, int* ch) {
     if (s->samples < 0) return fail(RT_ERR_INVALID, "samples %d", s->samples);
     if (s->precision != RT_PREC_F64 && s->precision != RT_PREC_F32) return fail(RT_ERR_INVALID, "precision %d", s->precision);
     if (s->aa_mode < 0 || s->aa_mode > 2) return fail(RT_ERR_INVALID, "aa_mode %d", s->aa_mode);
+    if (s->denoise && (*cw != s->width || *ch != s->height))
+        return fail(RT_ERR_INVALID, "denoise needs the full frame (PostProcessor.denoise clamps to the image edge)");
     return RT_OK;
+}
+
+// mean, toneMap, gammaCorrect (+ PostProcessor.denoise), RGBA8 on `st` (ray-tracer.js:208-276)
+hipError_t epilogue(rt_scene* sc, const rt_settings* s, int cw, int ch, const double* sum, double* mean, float* post,
+                    uint8_t* rgba, hipStream_t st) {
+    FinalizeParams fp{cw * ch, s->samples, s->tone_map, s->exposure, s->gamma};
+    if (!s->denoise) return launch_finalize(fp, sum, mean, post, rgba, st);
+    hipError_t e = sc->post_raw.ensure(4 * (size_t)cw * ch);
+    if (e == hipSuccess) e = launch_finalize(fp, sum, mean, sc->post_raw.p, nullptr, st);
+    if (e == hipSuccess) e = launch_denoise(cw, ch, s->denoise_weights[0], s->denoise_weights[1], sc->post_raw.p, post, rgba, st);
+    return e;
 }
 
 ImageParams image_params(const rt_settings* s, int cw, int ch) {
@@ -234,7 +247,7 @@ void rt_scene_destroy(rt_scene* sc) {
     if (sc->stream) (void)hipStreamSynchronize(sc->stream);
     sc->s64.release();
     sc->s32.release();
-    sc->sum.release(); sc->mean.release(); sc->post.release(); sc->rgba.release();
+    sc->sum.release(); sc->mean.release(); sc->post.release(); sc->post_raw.release(); sc->rgba.release();
     sc->segs.release(); sc->draws.release(); sc->total.release();
     for (auto& e : sc->ev)
         if (e) (void)hipEventDestroy(e);
@@ -294,14 +307,13 @@ int rt_render(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progr
         }
         if (sc->cancel.load()) return fail(RT_ERR_CANCELLED, "render cancelled after %d samples", bi.s_end);
     }
-    FinalizeParams fp{(int)n, s->samples, s->tone_map, s->exposure, s->gamma};
     const bool want_mean = out && out->mean, want_post = out && out->post, want_rgba = out && out->rgba8;
     if (want_mean) HIP_TRY(sc->mean.ensure(3 * n));
     if (want_post) HIP_TRY(sc->post.ensure(4 * n));
     if (want_rgba) HIP_TRY(sc->rgba.ensure(4 * n));
     HIP_TRY(hipEventRecord(sc->ev[2], sc->stream));
-    HIP_TRY(launch_finalize(fp, sc->sum.p, want_mean ? sc->mean.p : nullptr, want_post ? sc->post.p : nullptr,
-                            want_rgba ? sc->rgba.p : nullptr, sc->stream));
+    HIP_TRY(epilogue(sc, s, cw, ch, sc->sum.p, want_mean ? sc->mean.p : nullptr, want_post ? sc->post.p : nullptr,
+                     want_rgba ? sc->rgba.p : nullptr, sc->stream));
     HIP_TRY(hipEventRecord(sc->ev[3], sc->stream));
     if (want_mean) HIP_TRY(hipMemcpyAsync(out->mean, sc->mean.p, 3 * n * sizeof(double), hipMemcpyDeviceToHost, sc->stream));
     if (want_post) HIP_TRY(hipMemcpyAsync(out->post, sc->post.p, 4 * n * sizeof(float), hipMemcpyDeviceToHost, sc->stream));
@@ -360,14 +372,14 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
     return RT_OK;
 }
 
-int rt_finalize_device(const rt_settings* s, const double* d_sum, double* d_mean, float* d_post, uint8_t* d_rgba8,
-                       void* hip_stream) {
+int rt_finalize_device(rt_scene* sc, const rt_settings* s, const double* d_sum, double* d_mean, float* d_post,
+                       uint8_t* d_rgba8, void* hip_stream) {
+    if (!sc || !d_sum) return fail(RT_ERR_INVALID, "NULL argument");
     int cw, ch;
     int rc = check_settings(s, &cw, &ch);
     if (rc) return rc;
-    if (!d_sum) return fail(RT_ERR_INVALID, "d_sum is NULL");
-    FinalizeParams fp{cw * ch, s->samples, s->tone_map, s->exposure, s->gamma};
-    HIP_TRY(launch_finalize(fp, d_sum, d_mean, d_post, d_rgba8, (hipStream_t)hip_stream));
+    HIP_TRY(hipSetDevice(sc->device));
+    HIP_TRY(epilogue(sc, s, cw, ch, d_sum, d_mean, d_post, d_rgba8, (hipStream_t)hip_stream));
     return RT_OK;
 }
 

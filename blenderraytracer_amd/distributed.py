@@ -72,6 +72,6 @@ class ShardedRender:
         reduce_sums(self.sum, self.world, self.group)
         if self.rank == 0 and self._trace is None:
             stream = torch.cuda.current_stream(self.device)
-            capi.check(self.lib.rt_finalize_device(C.byref(self.full_settings), C.c_void_p(self.sum.data_ptr()), None,
+            capi.check(self.lib.rt_finalize_device(self.scene, C.byref(self.full_settings), C.c_void_p(self.sum.data_ptr()), None,
                                                    C.c_void_p(self.post.data_ptr()), C.c_void_p(self.rgba8.data_ptr()),
                                                    C.c_void_p(stream.cuda_stream)))

@@ -46,6 +46,10 @@ export function settingsOf(rt, opts = {}) {
         cropX0: opts.crop ? opts.crop[0] : 0, cropY0: opts.crop ? opts.crop[1] : 0,
         cropW: opts.crop ? opts.crop[2] : 0, cropH: opts.crop ? opts.crop[3] : 0,
         wantMean: opts.wantMean ? 1 : 0, wantCounts: opts.wantCounts ? 1 : 0,
+        // PostProcessor.denoise weights, evaluated with V8's Math.exp exactly as post-processor.js:55 does
+        denoise: rt.denoising ? 1 : 0,
+        denoiseW1: Math.exp(-(1) / (2 * rt.denoiseStrength * rt.denoiseStrength)),
+        denoiseW2: Math.exp(-(2) / (2 * rt.denoiseStrength * rt.denoiseStrength)),
     };
 }
 
@@ -71,20 +75,15 @@ export async function gpuRender(rt, onProgress, opts = {}) {
 }
 
 function blit(rt, res) {
-    // ray-tracer.js:215-252: RGBA8 top-down row-major, alpha 255 (computed on the GPU)
+    // ray-tracer.js:215-276: RGBA8 top-down row-major, alpha 255, denoised when rt.denoising (all on the GPU)
     rt.imageData.data.set(res.rgba8);
     rt.floatData = res.post;
     if (rt.ctx && rt.ctx.putImageData) rt.ctx.putImageData(rt.imageData, 0, 0);
 }
 
-function checkSupported(rt) {
-    if (rt.denoising) throw new Error('denoising is not yet on the GPU path (SURVEY §8f rank 1)');
-}
-
 // Option 1: swap the render() of a reference RayTracer instance for the GPU path.
 export function installGpuRender(rayTracer, opts = {}) {
     rayTracer.render = async function render(onProgress) {
-        checkSupported(this);
         const res = await gpuRender(this, onProgress, opts);
         if (!res) return;
         blit(this, res);
@@ -148,7 +147,6 @@ export class GpuRayTracer {
     }
 
     async render(onProgress) {
-        checkSupported(this);
         const res = await gpuRender(this, onProgress, this.opts);
         if (!res) return;
         blit(this, res);

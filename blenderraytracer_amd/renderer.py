@@ -7,15 +7,17 @@ update_background (:568-585), resize_canvas (:598-614), render(on_progress) (:16
 Randomness: Math.random is replaced by the keyed RNG; `seed` selects the stream.
 """
 import ctypes as C
+import math
 
 import numpy as np
 
 from . import capi
-from .scene import PackedScene, default_scene, load_from_json, setup_camera, keyed_permutation, js_or
+from .scene import PackedScene, default_scene, load_from_json, setup_camera, keyed_permutation, js_or, truthy
 
 
 def settings_struct(width, height, samples, max_bounces, anti_aliasing, tone_mapping, exposure, gamma, seed,
-                    crop=None, precision=capi.RT_PREC_F64, sample_range=None, batch_samples=0):
+                    crop=None, precision=capi.RT_PREC_F64, sample_range=None, batch_samples=0, denoising=False,
+                    denoise_strength=0.5):
     """rt_settings from RayTracer fields, resolving sampleCount (ray-tracer.js:201) and the string
     switches of getAntiAliasSample (:125-149) and toneMap (:151-161)."""
     s = capi.Settings()
@@ -33,6 +35,11 @@ def settings_struct(width, height, samples, max_bounces, anti_aliasing, tone_map
         s.crop_x0, s.crop_y0, s.crop_w, s.crop_h = (int(v) for v in crop)
     s.precision = int(precision)
     s.batch_samples = int(batch_samples)
+    if truthy(denoising):
+        # post-processor.js:55: Math.exp(-(kx*kx + ky*ky) / (2 * strength * strength)) for kx^2+ky^2 = 1, 2
+        st = float(denoise_strength)
+        s.denoise = 1
+        s.denoise_weights[:] = (math.exp(-1 / (2 * st * st)), math.exp(-2 / (2 * st * st)))
     return s
 
 
@@ -101,7 +108,8 @@ class GpuRayTracer:
     def settings(self, crop=None, sample_range=None, batch_samples=0):
         return settings_struct(self.width, self.height, self.samples, self.max_bounces, self.anti_aliasing,
                                self.tone_mapping, self.exposure, self.gamma, self.seed, crop=crop,
-                               precision=self.precision, sample_range=sample_range, batch_samples=batch_samples)
+                               precision=self.precision, sample_range=sample_range, batch_samples=batch_samples,
+                               denoising=self.denoising, denoise_strength=self.denoise_strength)
 
     def scene_handle(self):
         lib = capi.load_library()

@@ -135,14 +135,18 @@ typedef struct rt_settings {
     int32_t crop_w, crop_h;
     int32_t precision;         /* rt_precision */
     int32_t batch_samples;     /* samples per launch (progress/cancel granularity); 0 = all   */
-    int32_t _pad;
+    int32_t denoise;           /* this.denoising: PostProcessor.denoise after gamma (ray-tracer.js:266-276);
+                                  needs the full frame (crop_w/h = 0 or the whole image) */
+    double denoise_weights[2]; /* Math.exp(-1/(2s*s)), Math.exp(-2/(2s*s)), s = denoiseStrength, evaluated by
+                                  the host with its own exp (post-processor.js:55) */
 } rt_settings;
 
 /* Host outputs of rt_render, each optional (NULL = not wanted). n = crop_w*crop_h pixels,
  * top-down row-major like imageData. */
 typedef struct rt_output {
     double* mean;          /* n*3: per-pixel linear mean, the toneMap() input (ray-tracer.js:208) */
-    float* post;           /* n*4: post-gamma floats + alpha 1.0 (the floatData of ray-tracer.js:216-219) */
+    float* post;           /* n*4: post-gamma floats + alpha 1.0 (the floatData of ray-tracer.js:216-219);
+                              with denoise: the denoised floats the RGBA8 bytes are made from */
     uint8_t* rgba8;        /* n*4: min(255,max(0,floor(c*255))), NaN -> 0, alpha 255 (ray-tracer.js:226-252) */
     uint32_t* segments;    /* n: world.hit calls per pixel (diagnostic; enables device counting) */
     uint32_t* draws;       /* n: RNG draws per pixel (diagnostic) */
@@ -185,10 +189,11 @@ int rt_render(rt_scene* scene, const rt_settings* settings, const rt_output* out
 int rt_trace_device(rt_scene* scene, const rt_settings* settings, double* d_sum, void* hip_stream,
                     int sync, rt_stats* stats);
 
-/* Epilogue on device: mean = sum / sampleCount, toneMap, gammaCorrect, RGBA8 (ray-tracer.js:208-252).
- * Any output pointer may be NULL. All pointers are device pointers. */
-int rt_finalize_device(const rt_settings* settings, const double* d_sum, double* d_mean, float* d_post,
-                       uint8_t* d_rgba8, void* hip_stream);
+/* Epilogue on device: mean = sum / sampleCount, toneMap, gammaCorrect, optional denoise, RGBA8
+ * (ray-tracer.js:208-276).  Any output pointer may be NULL.  All pointers are device pointers; the
+ * scene provides the scratch buffer the denoise pass reads from. */
+int rt_finalize_device(rt_scene* scene, const rt_settings* settings, const double* d_sum, double* d_mean,
+                       float* d_post, uint8_t* d_rgba8, void* hip_stream);
 
 /* Request cancellation of an in-flight rt_render on `scene` (polled between sample batches). */
 int rt_cancel(rt_scene* scene);

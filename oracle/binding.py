@@ -46,6 +46,8 @@ def lib():
         L.orc_tone_map.restype = None
         L.orc_gamma.argtypes = [C.c_double, dp, dp]
         L.orc_gamma.restype = None
+        L.orc_denoise.argtypes = [C.POINTER(C.c_float), C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_float)]
+        L.orc_denoise.restype = None
         L.orc_rng_draw.argtypes = [C.c_uint32] * 4
         L.orc_rng_draw.restype = C.c_double
         _lib = L
@@ -54,6 +56,20 @@ def lib():
 
 def _p(a, t=C.c_double):
     return None if a is None else a.ctypes.data_as(C.POINTER(t))
+
+
+def denoise(post, settings):
+    """PostProcessor.denoise of the post-gamma frame (stored as Float32 like floatData) -> (floats, rgba8)."""
+    h, w = post.shape[:2]
+    fl = np.ones((h, w, 4), dtype=np.float32)
+    fl[..., :3] = post
+    out = np.zeros_like(fl)
+    wts = np.array(list(settings.denoise_weights), dtype=np.float64)
+    lib().orc_denoise(fl.ctypes.data_as(C.POINTER(C.c_float)), w, h, _p(wts), out.ctypes.data_as(C.POINTER(C.c_float)))
+    v = np.floor(out[..., :3].astype(np.float64) * 255)
+    rgba = np.full((h, w, 4), 255, dtype=np.uint8)
+    rgba[..., :3] = np.where(np.isnan(v), 0, np.clip(v, 0, 255)).astype(np.uint8)
+    return out, rgba
 
 
 def render(packed, settings):
@@ -68,4 +84,7 @@ def render(packed, settings):
     draws = np.zeros((ch, cw), dtype=np.uint32)
     lib().orc_render(C.byref(packed.desc), C.byref(settings), _p(mean), _p(post), _p(rgba, C.c_uint8),
                      _p(segs, C.c_uint32), _p(draws, C.c_uint32))
-    return {"mean": mean, "post": post, "rgba8": rgba, "segments": segs, "draws": draws}
+    res = {"mean": mean, "post": post, "rgba8": rgba, "segments": segs, "draws": draws}
+    if settings.denoise:
+        res["denoised"], res["rgba8"] = denoise(post, settings)
+    return res

@@ -503,3 +503,29 @@ double orc_rng_draw(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t k) 
     Rng rng = {sample_key(seed_mix(seed), pixel, sample), k, NULL};
     return rng_next(&rng);
 }
+
+/* PostProcessor.denoise (post-processor.js:45-77) over a Float32 RGBA frame, binary64 accumulation in
+ * the reference's order; weights w[0] = exp(-1/(2s*s)), w[1] = exp(-2/(2s*s)) come from the caller. */
+void orc_denoise(const float* in, int w, int h, const double* wts, float* out) {
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            double r = 0, g = 0, b = 0, weight = 0;
+            for (int ky = -1; ky <= 1; ky++)
+                for (int kx = -1; kx <= 1; kx++) {
+                    int nx = x + kx < 0 ? 0 : (x + kx > w - 1 ? w - 1 : x + kx);
+                    int ny = y + ky < 0 ? 0 : (y + ky > h - 1 ? h - 1 : y + ky);
+                    size_t idx = ((size_t)ny * w + nx) * 4;
+                    int d2 = kx * kx + ky * ky;
+                    double wt = d2 == 0 ? 1.0 : wts[d2 - 1];
+                    r += in[idx] * wt;
+                    g += in[idx + 1] * wt;
+                    b += in[idx + 2] * wt;
+                    weight += wt;
+                }
+            size_t idx = ((size_t)y * w + x) * 4;
+            out[idx] = (float)(r / weight);
+            out[idx + 1] = (float)(g / weight);
+            out[idx + 2] = (float)(b / weight);
+            out[idx + 3] = in[idx + 3];
+        }
+}

@@ -124,6 +124,11 @@ async function runCase(mods, c) {
     world.hit = (ray, a, b) => { fullSegs[curPix]++; return origHit(ray, a, b); };
 
     const sampleCount = rt.antiAliasing === 'none' ? 1 : rt.samples;
+    // PostProcessor.denoise (post-processor.js:45-77) output, when render() applies it (ray-tracer.js:266-276)
+    let denoised = null;
+    const PP = mods.PostProcessor;
+    const origDenoise = PP.denoise;
+    PP.denoise = (data, w, h, strength) => { denoised = origDenoise.call(PP, data, w, h, strength); return denoised; };
     const t0 = process.hrtime.bigint();
     if (!c.crop) {
         await rt.render();
@@ -154,6 +159,7 @@ async function runCase(mods, c) {
         }
     }
     const secs = Number(process.hrtime.bigint() - t0) / 1e9;
+    PP.denoise = origDenoise;
     drawCounter = null; curPix = -1;
     for (let r = 0; r < ch; r++) for (let x = 0; x < cw; x++) {
         const p = (y0 + r) * W + (x0 + x);
@@ -161,7 +167,9 @@ async function runCase(mods, c) {
     }
     const cam = rt.camera;
     const files = {};
-    for (const [k, arr] of Object.entries({ linear, post, rgba8: rgba, segs, draws })) {
+    const arrays = { linear, post, rgba8: rgba, segs, draws };
+    if (denoised) arrays.denoised = denoised;
+    for (const [k, arr] of Object.entries(arrays)) {
         files[k] = `${c.name}.${k}.gz`;
         writeGz(files[k], arr);
     }
@@ -171,6 +179,7 @@ async function runCase(mods, c) {
         resolved: {
             maxBounces: rt.maxBounces, samples: rt.samples, gamma: rt.gamma, exposure: rt.exposure,
             toneMapping: rt.toneMapping, antiAliasing: rt.antiAliasing, denoising: rt.denoising,
+            denoiseStrength: rt.denoiseStrength,
             skyIntensity: rt.world.skyIntensity,
         },
         camera: {

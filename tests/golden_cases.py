@@ -28,12 +28,17 @@ def case_names():
 
 def load_array(case, key):
     c = manifest()["cases"][case]
-    dt = {"linear": np.float64, "post": np.float64, "rgba8": np.uint8, "segs": np.uint32, "draws": np.uint32}[key]
+    dt = {"linear": np.float64, "post": np.float64, "rgba8": np.uint8, "segs": np.uint32, "draws": np.uint32,
+          "denoised": np.float32}[key]
     raw = gzip.open(os.path.join(GOLDEN, c["files"][key])).read()
     _, _, cw, ch = c["crop"]
-    comp = {"linear": 3, "post": 3, "rgba8": 4, "segs": 1, "draws": 1}[key]
+    comp = {"linear": 3, "post": 3, "rgba8": 4, "segs": 1, "draws": 1, "denoised": 4}[key]
     a = np.frombuffer(raw, dtype=dt).reshape(ch, cw, comp)
     return a[..., 0] if comp == 1 else a
+
+
+def has(case, key):
+    return key in manifest()["cases"][case]["files"]
 
 
 def kats():

@@ -87,6 +87,9 @@ def check_against_python(name, d):
         (st.width, st.height, st.samples, st.max_depth, st.aa_mode, st.tone_map), name
     assert (js["exposure"], js["gamma"], js["seed"]) == (st.exposure, st.gamma, st.seed)
     assert (js["cropX0"], js["cropY0"], js["cropW"], js["cropH"]) == (st.crop_x0, st.crop_y0, st.crop_w, st.crop_h)
+    assert js["denoise"] == st.denoise
+    if st.denoise:   # V8 Math.exp vs glibc exp: equal or 1 ulp apart
+        assert np.allclose([js["denoiseW1"], js["denoiseW2"]], list(st.denoise_weights), rtol=4e-16, atol=0)
 
 
 def test_js_packing_matches_python_host():

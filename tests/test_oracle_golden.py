@@ -24,7 +24,10 @@ def test_oracle_matches_reference(case):
     assert np.all(np.abs(r["mean"][ok] - lin[ok]) <= tol), "linear mean differs from the reference"
     okp = ~np.isnan(post)
     assert np.all(np.abs(r["post"][okp] - post[okp]) <= 4 * np.spacing(np.abs(post[okp])) + 1e-300)
-    assert np.array_equal(r["rgba8"], gc.load_array(case, "rgba8"))
+    assert np.array_equal(r["rgba8"], gc.load_array(case, "rgba8"))     # denoised when the case denoises
+    if gc.has(case, "denoised"):
+        dn = gc.load_array(case, "denoised")
+        assert np.all(np.abs(r["denoised"] - dn) <= np.spacing(np.abs(dn))), "PostProcessor.denoise differs"
     assert np.array_equal(r["segments"], gc.load_array(case, "segs")), "world.hit counts differ"
     assert np.array_equal(r["draws"], gc.load_array(case, "draws")), "Math.random draw counts differ"
 
