@@ -54,14 +54,18 @@ def parse():
     ap.add_argument("--config", default="rtow", choices=sorted(CONFIGS))
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--accel", default="auto", choices=["auto", "brute", "bvh"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-crop", type=int, default=64, help="side of the square crop the CPU oracle renders")
     return ap.parse_args()
 
 
-def make_tracer(cfg, precision, seed, device):
+ACCEL = {"auto": capi.RT_ACCEL_AUTO, "brute": capi.RT_ACCEL_BRUTE, "bvh": capi.RT_ACCEL_BVH}
+
+
+def make_tracer(cfg, precision, seed, device, accel="auto"):
     rt = GpuRayTracer(cfg["w"], cfg["h"], seed=seed, device=device,
-                      precision=capi.RT_PREC_F64 if precision == "f64" else capi.RT_PREC_F32)
+                      precision=capi.RT_PREC_F64 if precision == "f64" else capi.RT_PREC_F32, accel=ACCEL[accel])
     assert rt.load_from_json(load_scene_json(cfg["scene"]))
     if (rt.width, rt.height) != (cfg["w"], cfg["h"]):
         rt.resize_canvas(cfg["w"], cfg["h"])
@@ -106,7 +110,7 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    rt = make_tracer(cfg, args.precision, args.seed, local)
+    rt = make_tracer(cfg, args.precision, args.seed, local, args.accel)
     packed = rt.packed()
     flops_per_segment = sum(FLOPS[k] * (o.count if k in ("mesh", "triangle") else 1)
                             for k, o in zip(packed.kinds, packed.objects))
@@ -154,7 +158,7 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"config{cfg['cfg']}_{args.config}_{cfg['w']}x{cfg['h']}_{cfg['spp']}spp",
                        "scene": cfg["scene"], "width": cfg["w"], "height": cfg["h"], "spp": cfg["spp"],
-                       "max_depth": cfg["depth"], "primitives": packed.primitives_per_segment(),
+                       "max_depth": cfg["depth"], "primitives": packed.primitives_per_segment(), "accel": args.accel,
                        "parallelism": f"sample-split x{world} + RCCL reduce" if world > 1 else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),

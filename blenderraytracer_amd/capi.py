@@ -19,6 +19,7 @@ RT_CAM_PERSPECTIVE, RT_CAM_ORTHOGRAPHIC = range(2)
 RT_AA_SUPERSAMPLING, RT_AA_STOCHASTIC, RT_AA_CENTER = range(3)
 RT_TM_REINHARD, RT_TM_ACES, RT_TM_LINEAR = range(3)
 RT_PREC_F64, RT_PREC_F32 = range(2)
+RT_ACCEL_AUTO, RT_ACCEL_BRUTE, RT_ACCEL_BVH = range(3)
 
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_DEVICE", -3: "RT_ERR_NOMEM",
           -4: "RT_ERR_CANCELLED", -5: "RT_ERR_NO_DEVICE"}
@@ -54,7 +55,7 @@ class Settings(C.Structure):
                 ("seed", C.c_uint32), ("sample_begin", C.c_int32), ("sample_end", C.c_int32),
                 ("crop_x0", C.c_int32), ("crop_y0", C.c_int32), ("crop_w", C.c_int32), ("crop_h", C.c_int32),
                 ("precision", C.c_int32), ("batch_samples", C.c_int32), ("denoise", C.c_int32),
-                ("denoise_weights", C.c_double * 2)]
+                ("denoise_weights", C.c_double * 2), ("accel", C.c_int32), ("_pad", C.c_int32)]
 
 
 class Output(C.Structure):

@@ -296,6 +296,7 @@ napi_value render(napi_env env, napi_callback_info info) {
     st.precision = (int32_t)get_num(env, s, "precision", RT_PREC_F64);
     st.batch_samples = (int32_t)get_num(env, s, "batchSamples", 0);
     st.denoise = (int32_t)get_num(env, s, "denoise", 0);
+    st.accel = (int32_t)get_num(env, s, "accel", RT_ACCEL_AUTO);
     st.denoise_weights[0] = get_num(env, s, "denoiseW1", 0.0);
     st.denoise_weights[1] = get_num(env, s, "denoiseW2", 0.0);
     job->want_mean = get_num(env, s, "wantMean", 0) != 0;

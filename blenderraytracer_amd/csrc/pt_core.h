@@ -75,6 +75,12 @@ template <class R> struct BoxRec { R mnx, mny, mnz, mxx, mxy, mxz; };
 template <class R> struct TriRec { R v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z, nx, ny, nz; };  // e1=v1-v0, e2=v2-v0
 template <class R> struct MatRec { int type, pad; R albedo[3]; R rough; R ior; R emit[3]; };
 
+// BVH node (32 B), nodes in depth-first preorder: an internal node's first child is the next node,
+// `skip` is the index just past its subtree.  fc = (first << 4) | count for a leaf of `count` <= 15
+// primitives at leaf-order positions [first, first+count), 0 for an internal node.
+struct BvhNode { float lo[3]; int skip; float hi[3]; int fc; };
+struct PrimKey { int id, obj; };   // index into the World-order arrays, World.objects index
+
 template <class R>
 struct SceneView {
     const Run* runs;
@@ -93,6 +99,20 @@ struct SceneView {
     const int* tri_mat;            // per triangle (mesh triangles carry the mesh's material)
     const MatRec<R>* mats;
     const int* perm;               // World.cloudNoise.p[512]
+    // acceleration structure (closest_hit_bvh): planes and boxes are tested brute force with their
+    // World.objects index, spheres and triangles through one BVH each over leaf-order copies
+    int num_planes, num_boxes;
+    const int* plane_obj;
+    const int* box_obj;
+    const BvhNode* sphere_nodes;
+    int num_sphere_nodes;
+    const SphereRec<R>* bvh_spheres;
+    const SphereFilter* bvh_sphere_filter;
+    const PrimKey* bvh_sphere_key;
+    const BvhNode* tri_nodes;
+    int num_tri_nodes;
+    const TriRec<R>* bvh_tris;
+    const PrimKey* bvh_tri_key;
     // camera (camera.js:8-36 vectors, computed on the host in binary64)
     R cam_o[3], cam_llc[3], cam_h[3], cam_v[3], cam_u[3], cam_vv[3], cam_w[3];
     R lens_radius;
@@ -105,7 +125,7 @@ struct SceneView {
 enum HitKind : int { HIT_NONE = -1, HIT_SPHERE = 0, HIT_PLANE = 1, HIT_BOX = 2, HIT_TRI = 3 };
 
 template <class R>
-struct Closest { R t; int kind, idx, mat; };
+struct Closest { R t; int kind, idx, mat, obj; };   // obj: World.objects index (BVH mode only)
 
 // Filter records staged in LDS by the workgroup (pt_trace.hip), read by every lane at the same
 // address (broadcast ds_read_b128).
@@ -255,6 +275,183 @@ RT_UNROLL(RT_SPHERE_UNROLL)
         }
     }
     return b;
+}
+
+// ---- BVH mode ---------------------------------------------------------------------------------------
+// World.hit's result is the minimum of a total order over the candidates: every object's candidate t
+// is independent of tMax (a sphere takes its near root if >= tMin, else its far root; the far root
+// is never below the near one), World.hit accepts strictly smaller t (the first of equal t wins) and
+// a mesh accepts <= (the last equal-t triangle wins, geometry.js:253-259).  So the winner is the
+// least (t, World.objects index ascending, triangle index descending) — order-independent, which lets
+// a BVH visit primitives in any order and stay bit-identical to the brute-force walk.  NaN
+// candidates never win, nor does +inf (World.hit starts from closestT = Infinity).
+template <class R>
+RT_HD bool better(R t, int obj, int id, const Closest<R>& b) {
+    return t < b.t || (t == b.t && (obj < b.obj || (obj == b.obj && id > b.idx)));
+}
+
+template <class R>
+RT_HD bool sphere_candidate(const SphereRec<R>& s, V3<R> o, V3<R> d, R a, R tmin, R& t) {   // geometry.js:15-45
+    R ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
+    R hb = ocx * d.x + ocy * d.y + ocz * d.z;
+    R c = (ocx * ocx + ocy * ocy + ocz * ocz) - s.r2;
+    R disc = hb * hb - a * c;
+    if (disc < (R)0) return false;
+    R sq = sqrt(disc);
+    t = (-hb - sq) / a;
+    if (!(t < tmin)) return true;
+    t = (-hb + sq) / a;
+    return !(t < tmin);
+}
+
+template <class R>
+RT_HD bool triangle_candidate(const TriRec<R>& tr, V3<R> o, V3<R> d, R tmin, R& t) {   // geometry.js:148-188
+    R hx = d.y * tr.e2z - d.z * tr.e2y, hy = d.z * tr.e2x - d.x * tr.e2z, hz = d.x * tr.e2y - d.y * tr.e2x;
+    R aa = tr.e1x * hx + tr.e1y * hy + tr.e1z * hz;
+    if (fabs(aa) < (R)0.0001) return false;
+    R f = (R)1 / aa;
+    R sx = o.x - tr.v0x, sy = o.y - tr.v0y, sz = o.z - tr.v0z;
+    R u = f * (sx * hx + sy * hy + sz * hz);
+    if (u < (R)0 || u > (R)1) return false;
+    R qx = sy * tr.e1z - sz * tr.e1y, qy = sz * tr.e1x - sx * tr.e1z, qz = sx * tr.e1y - sy * tr.e1x;
+    R v = f * (d.x * qx + d.y * qy + d.z * qz);
+    if (v < (R)0 || u + v > (R)1) return false;
+    t = f * (tr.e2x * qx + tr.e2y * qy + tr.e2z * qz);
+    return !(t < tmin);
+}
+
+// bvh_conservative_bound.  A primitive accepted at parameter t has its computed hit point within
+// 2^-25 (|o| + |c|) of the primitive's bounding box (the worst case is a near-tangent sphere root,
+// whose error is sqrt(u) relative), far inside the node inflation 2^-19 max|bound| (scene_pack.h)
+// plus the per-ray origin pad 2^-19 |o|_inf below.  The binary32 slab test then errs by < 2^-22 of
+// |bound - o| per axis (rounded o, d, 1/d and the product), which the same margins cover, and the
+// ray-length limit is (float)t_best rounded up by 2^-20.  So a node holding a primitive that beats
+// the current best is never culled; f64 mode stays bit-identical to the brute-force walk
+// (tests/test_hostcheck.py, tests/test_gpu_parity.py).  Directions with a binary32-denormal
+// component are clamped to 1/d = 2^126 (t ranges beyond 2^100 are not modelled).
+struct BvhRay { float olo[3], ohi[3], inv[3]; };
+
+template <class R>
+RT_HD BvhRay make_bvh_ray(V3<R> o, V3<R> d) {
+    BvhRay r;
+    const float of[3] = {(float)o.x, (float)o.y, (float)o.z};
+    const float df[3] = {(float)d.x, (float)d.y, (float)d.z};
+    const float m = fmaxf(fabsf(of[0]), fmaxf(fabsf(of[1]), fabsf(of[2])));
+    const float pad = m * (0x1p-19f * (1.0f + 0x1p-20f)) + 0x1p-100f;
+    for (int k = 0; k < 3; ++k) {
+        r.olo[k] = of[k] + pad;      // (lo - olo) * inv and (hi - ohi) * inv widen the slab for both signs of d
+        r.ohi[k] = of[k] - pad;
+        float inv = 1.0f / df[k];
+        if (!(fabsf(inv) <= 0x1p126f)) inv = copysignf(0x1p126f, df[k]);
+        r.inv[k] = inv;
+    }
+    return r;
+}
+
+template <class R>
+RT_HD float bvh_tlimit(R t) {   // >= t, +inf while nothing was hit
+    return (float)t * (1.0f + 0x1p-20f);
+}
+
+RT_HD bool bvh_node_hit(const BvhNode& n, const BvhRay& r, float tlimit) {
+    const float x0 = (n.lo[0] - r.olo[0]) * r.inv[0], x1 = (n.hi[0] - r.ohi[0]) * r.inv[0];
+    const float y0 = (n.lo[1] - r.olo[1]) * r.inv[1], y1 = (n.hi[1] - r.ohi[1]) * r.inv[1];
+    const float z0 = (n.lo[2] - r.olo[2]) * r.inv[2], z1 = (n.hi[2] - r.ohi[2]) * r.inv[2];
+    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.0f));
+    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tlimit));
+    return tn <= tf;
+}
+
+// Closest hit through the BVHs: planes and boxes (usually few, often large) brute force first, then
+// the sphere BVH and the triangle BVH, each a stackless walk of the preorder node array.  Lanes walk
+// their own paths (per-lane node loads); leaf records are contiguous in leaf order.
+template <class R>
+RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d) {
+    const R tmin = (R)0.001;
+    Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
+    for (int i = 0; i < sc.num_planes; ++i) {                                 // geometry.js:56-74
+        const PlaneRec<R> p = sc.planes[i];
+        R denom = p.nx * d.x + p.ny * d.y + p.nz * d.z;
+        if (fabs(denom) < (R)1e-6) continue;
+        R t = ((p.px - o.x) * p.nx + (p.py - o.y) * p.ny + (p.pz - o.z) * p.nz) / denom;
+        if (t < tmin) continue;
+        const int obj = sc.plane_obj[i];
+        if (better(t, obj, i, b)) b = Closest<R>{t, HIT_PLANE, i, sc.plane_mat[i], obj};
+    }
+    for (int i = 0; i < sc.num_boxes; ++i) {                                  // geometry.js:85-117
+        const BoxRec<R> bx = sc.boxes[i];
+        R t0 = (bx.mnx - o.x) / d.x, t1 = (bx.mxx - o.x) / d.x;
+        if (t0 > t1) { R s = t0; t0 = t1; t1 = s; }
+        R ty0 = (bx.mny - o.y) / d.y, ty1 = (bx.mxy - o.y) / d.y;
+        if (ty0 > ty1) { R s = ty0; ty0 = ty1; ty1 = s; }
+        if (t0 > ty1 || ty0 > t1) continue;
+        t0 = js_max(t0, ty0);
+        t1 = js_min(t1, ty1);
+        R tz0 = (bx.mnz - o.z) / d.z, tz1 = (bx.mxz - o.z) / d.z;
+        if (tz0 > tz1) { R s = tz0; tz0 = tz1; tz1 = s; }
+        if (t0 > tz1 || tz0 > t1) continue;
+        t0 = js_max(t0, tz0);
+        t1 = js_min(t1, tz1);
+        R t = t0 > tmin ? t0 : t1;
+        if (t < tmin) continue;
+        const int obj = sc.box_obj[i];
+        if (better(t, obj, i, b)) b = Closest<R>{t, HIT_BOX, i, sc.box_mat[i], obj};
+    }
+    const BvhRay br = make_bvh_ray(o, d);
+    float tl = bvh_tlimit(b.t);
+    if (sc.num_sphere_nodes > 0) {
+        const R a = dot(d, d);
+        FilterRay fr{};
+        if constexpr (sizeof(R) == 8) fr = make_filter_ray(o, d);
+        int ni = 0;
+        while (ni < sc.num_sphere_nodes) {
+            const BvhNode n = sc.sphere_nodes[ni];
+            if (!bvh_node_hit(n, br, tl)) { ni = n.skip; continue; }
+            if (n.fc == 0) { ++ni; continue; }
+            const int first = n.fc >> 4, end = first + (n.fc & 15);
+            for (int k = first; k < end; ++k) {
+                if constexpr (sizeof(R) == 8)
+                    if (!sphere_filter_pass(sc.bvh_sphere_filter[k], fr)) continue;
+                R t;
+                if (!sphere_candidate(sc.bvh_spheres[k], o, d, a, tmin, t)) continue;
+                const PrimKey key = sc.bvh_sphere_key[k];
+                if (better(t, key.obj, key.id, b)) {
+                    b = Closest<R>{t, HIT_SPHERE, key.id, sc.sphere_mat[key.id], key.obj};
+                    tl = bvh_tlimit(b.t);
+                }
+            }
+            ni = n.skip;
+        }
+    }
+    if (sc.num_tri_nodes > 0) {
+        int ni = 0;
+        while (ni < sc.num_tri_nodes) {
+            const BvhNode n = sc.tri_nodes[ni];
+            if (!bvh_node_hit(n, br, tl)) { ni = n.skip; continue; }
+            if (n.fc == 0) { ++ni; continue; }
+            const int first = n.fc >> 4, end = first + (n.fc & 15);
+            for (int k = first; k < end; ++k) {
+                R t;
+                if (!triangle_candidate(sc.bvh_tris[k], o, d, tmin, t)) continue;
+                const PrimKey key = sc.bvh_tri_key[k];
+                if (better(t, key.obj, key.id, b)) {
+                    b = Closest<R>{t, HIT_TRI, key.id, sc.tri_mat[key.id], key.obj};
+                    tl = bvh_tlimit(b.t);
+                }
+            }
+            ni = n.skip;
+        }
+    }
+    return b;
+}
+
+// acceleration modes of the trace kernel
+enum Accel : int { ACC_BRUTE = 0, ACC_LDS = 1, ACC_BVH = 2 };
+
+template <class R, int ACC>
+RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, const LdsSpheres lds) {
+    if constexpr (ACC == ACC_BVH) return closest_hit_bvh(sc, o, d);
+    else return closest_hit<R, ACC == ACC_LDS>(sc, o, d, lds);
 }
 
 template <class R>

@@ -15,7 +15,7 @@ struct Counters {
 };
 
 template <class R>
-hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, hipStream_t stream);
+hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh, hipStream_t stream);
 
 struct FinalizeParams {
     int n;

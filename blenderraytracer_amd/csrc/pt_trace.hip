@@ -22,11 +22,16 @@ struct TraceArgs {
 #define RT_MIN_WAVES_PER_SIMD 8   // 64 VGPRs: latency-bound loop, 8 waves/SIMD measured fastest
 #endif
 
-template <class R, bool COUNT, bool LDS>
-__global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void trace_kernel(const TraceArgs<R> args) {
+#ifndef RT_BVH_WAVES_PER_SIMD
+#define RT_BVH_WAVES_PER_SIMD 4   // the BVH walk keeps more live state: 128 VGPRs ("BVH")
+#endif
+
+template <class R, bool COUNT, int ACC>
+__global__ __launch_bounds__(256, ACC == ACC_BVH ? RT_BVH_WAVES_PER_SIMD : RT_MIN_WAVES_PER_SIMD)
+void trace_kernel(const TraceArgs<R> args) {
     const ImageParams& im = args.im;
     LdsSpheres lds{nullptr};
-    if constexpr (LDS) {
+    if constexpr (ACC == ACC_LDS) {
         // stage the binary32 sphere filter records of the whole scene in LDS (one copy per workgroup)
         extern __shared__ SphereFilter lds_spheres[];
         for (int t = threadIdx.x; t < args.sc.num_spheres; t += blockDim.x) lds_spheres[t] = args.sc.sphere_filter[t];
@@ -43,7 +48,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES_PER_SIMD) void trace_kernel(const
     double acc[3] = {0, 0, 0};
     if (valid) { acc[0] = args.c.sum[3 * q]; acc[1] = args.c.sum[3 * q + 1]; acc[2] = args.c.sum[3 * q + 2]; }
     // invalid lanes trace nothing but stay for the wave reduction below
-    const PixelResult r = trace_pixel<R, COUNT, LDS>(args.sc, im, cx, cy, valid ? im.s_end : im.s_begin, acc, lds);
+    const PixelResult r = trace_pixel<R, COUNT, ACC>(args.sc, im, cx, cy, valid ? im.s_end : im.s_begin, acc, lds);
     if (valid) {
         args.c.sum[3 * q] = acc[0]; args.c.sum[3 * q + 1] = acc[1]; args.c.sum[3 * q + 2] = acc[2];
         if (COUNT) {
@@ -69,31 +74,37 @@ static int sphere_path_override() {
     return v;
 }
 
+template <class R, int ACC>
+static void launch_acc(const TraceArgs<R>& a, int tiles, size_t lds_bytes, bool count, hipStream_t stream) {
+    if (count) hipLaunchKernelGGL((trace_kernel<R, true, ACC>), dim3(tiles), dim3(256), lds_bytes, stream, a);
+    else hipLaunchKernelGGL((trace_kernel<R, false, ACC>), dim3(tiles), dim3(256), lds_bytes, stream, a);
+}
+
 template <class R>
-hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, hipStream_t stream) {
+hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh,
+                        hipStream_t stream) {
     if (im.cw <= 0 || im.ch <= 0 || im.s_end <= im.s_begin) return hipSuccess;
     const int tiles = ((im.cw + 15) >> 4) * ((im.ch + 15) >> 4);
     TraceArgs<R> a{sc, im, c};
-    const size_t lds_bytes = (size_t)sc.num_spheres * sizeof(SphereFilter);
-    const int ov = sphere_path_override();
-    const bool lds = sizeof(R) == 8 && sc.num_spheres > 0 && lds_bytes <= 48 * 1024 && ov == 1;
     const bool count = c.segs || c.draws;
+    if (bvh) {
+        launch_acc<R, ACC_BVH>(a, tiles, 0, count, stream);
+        return hipGetLastError();
+    }
+    const size_t lds_bytes = (size_t)sc.num_spheres * sizeof(SphereFilter);
+    const bool lds = sizeof(R) == 8 && sc.num_spheres > 0 && lds_bytes <= 48 * 1024 && sphere_path_override() == 1;
     if constexpr (sizeof(R) == 8) {
         if (lds) {
-            if (count) hipLaunchKernelGGL((trace_kernel<R, true, true>), dim3(tiles), dim3(256), lds_bytes, stream, a);
-            else hipLaunchKernelGGL((trace_kernel<R, false, true>), dim3(tiles), dim3(256), lds_bytes, stream, a);
+            launch_acc<R, ACC_LDS>(a, tiles, lds_bytes, count, stream);
             return hipGetLastError();
         }
     }
-    {
-        if (count) hipLaunchKernelGGL((trace_kernel<R, true, false>), dim3(tiles), dim3(256), 0, stream, a);
-        else hipLaunchKernelGGL((trace_kernel<R, false, false>), dim3(tiles), dim3(256), 0, stream, a);
-    }
+    launch_acc<R, ACC_BRUTE>(a, tiles, 0, count, stream);
     return hipGetLastError();
 }
 
-template hipError_t launch_trace<double>(const SceneView<double>&, const ImageParams&, const Counters&, hipStream_t);
-template hipError_t launch_trace<float>(const SceneView<float>&, const ImageParams&, const Counters&, hipStream_t);
+template hipError_t launch_trace<double>(const SceneView<double>&, const ImageParams&, const Counters&, bool, hipStream_t);
+template hipError_t launch_trace<float>(const SceneView<float>&, const ImageParams&, const Counters&, bool, hipStream_t);
 
 // ---- epilogue: mean, toneMap, gammaCorrect, RGBA8 (ray-tracer.js:208-252, post-processor.js:9-42) ----
 __device__ __forceinline__ uint8_t to_u8(double c) {

@@ -83,10 +83,18 @@ struct DeviceScene {
     DevBuf<TriRec<R>> tris;
     DevBuf<int> sphere_mat, plane_mat, box_mat, tri_mat, perm;
     DevBuf<MatRec<R>> mats;
+    DevBuf<int> plane_obj, box_obj;
+    DevBuf<BvhNode> sphere_nodes, tri_nodes;
+    DevBuf<SphereRec<R>> bvh_spheres;
+    DevBuf<SphereFilter> bvh_sphere_filter;
+    DevBuf<PrimKey> bvh_sphere_key, bvh_tri_key;
+    DevBuf<TriRec<R>> bvh_tris;
     SceneView<R> view{};
     void release() {
         runs.release(); spheres.release(); sphere_filter.release(); sphere_r.release(); planes.release(); boxes.release(); tris.release();
         sphere_mat.release(); plane_mat.release(); box_mat.release(); tri_mat.release(); perm.release(); mats.release();
+        plane_obj.release(); box_obj.release(); sphere_nodes.release(); tri_nodes.release(); bvh_spheres.release();
+        bvh_sphere_filter.release(); bvh_sphere_key.release(); bvh_tri_key.release(); bvh_tris.release();
     }
 };
 
@@ -99,6 +107,9 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     UP(runs, hs.runs); UP(spheres, rec.spheres); UP(sphere_filter, rec.sphere_filter); UP(sphere_r, rec.sphere_r); UP(planes, rec.planes);
     UP(boxes, rec.boxes); UP(tris, rec.tris); UP(sphere_mat, hs.sphere_mat); UP(plane_mat, hs.plane_mat);
     UP(box_mat, hs.box_mat); UP(tri_mat, hs.tri_mat); UP(perm, rec.perm); UP(mats, rec.mats);
+    UP(plane_obj, hs.plane_obj); UP(box_obj, hs.box_obj); UP(sphere_nodes, hs.sphere_bvh); UP(tri_nodes, hs.tri_bvh);
+    UP(bvh_spheres, rec.bvh_spheres); UP(bvh_sphere_filter, rec.bvh_sphere_filter); UP(bvh_sphere_key, rec.bvh_sphere_key);
+    UP(bvh_tri_key, rec.bvh_tri_key); UP(bvh_tris, rec.bvh_tris);
 #undef UP
     if (e != hipSuccess) return fail(RT_ERR_DEVICE, "scene upload: %s", hipGetErrorString(e));
     SceneView<R>& v = ds.view;
@@ -106,6 +117,9 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     v.spheres = ds.spheres.p; v.sphere_filter = ds.sphere_filter.p; v.sphere_r = ds.sphere_r.p; v.planes = ds.planes.p; v.boxes = ds.boxes.p;
     v.tris = ds.tris.p; v.sphere_mat = ds.sphere_mat.p; v.plane_mat = ds.plane_mat.p; v.box_mat = ds.box_mat.p;
     v.tri_mat = ds.tri_mat.p; v.mats = ds.mats.p; v.perm = ds.perm.p;
+    v.plane_obj = ds.plane_obj.p; v.box_obj = ds.box_obj.p; v.sphere_nodes = ds.sphere_nodes.p; v.tri_nodes = ds.tri_nodes.p;
+    v.bvh_spheres = ds.bvh_spheres.p; v.bvh_sphere_filter = ds.bvh_sphere_filter.p; v.bvh_sphere_key = ds.bvh_sphere_key.p;
+    v.bvh_tris = ds.bvh_tris.p; v.bvh_tri_key = ds.bvh_tri_key.p;
     fill_view_constants(v, hs, d);
     return RT_OK;
 }
@@ -122,6 +136,7 @@ struct rt_scene {
     DeviceScene<double> s64;
     DeviceScene<float> s32;
     int num_prims = 0;
+    int bvh_prims = 0;              // spheres + triangles (the primitives the BVHs cover)
     double record_bytes = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {};
@@ -147,6 +162,7 @@ int check_settings(const rt_settings* s, int* cw, int* ch) {
     if (s->samples < 0) return fail(RT_ERR_INVALID, "samples %d", s->samples);
     if (s->precision != RT_PREC_F64 && s->precision != RT_PREC_F32) return fail(RT_ERR_INVALID, "precision %d", s->precision);
     if (s->aa_mode < 0 || s->aa_mode > 2) return fail(RT_ERR_INVALID, "aa_mode %d", s->aa_mode);
+    if (s->accel < RT_ACCEL_AUTO || s->accel > RT_ACCEL_BVH) return fail(RT_ERR_INVALID, "accel %d", s->accel);
     if (s->denoise && (*cw != s->width || *ch != s->height))
         return fail(RT_ERR_INVALID, "denoise needs the full frame (PostProcessor.denoise clamps to the image edge)");
     return RT_OK;
@@ -176,10 +192,15 @@ ImageParams image_params(const rt_settings* s, int cw, int ch) {
     return im;
 }
 
-hipError_t trace(rt_scene* sc, int precision, const ImageParams& im, const Counters& c, hipStream_t st) {
+// RT_ACCEL_AUTO: the BVH unless the scene has almost no spheres/triangles (measured faster from 10
+// primitives (Cornell) to 50k (mesh50k), DESIGN.md "BVH")
+constexpr int kAutoBvhPrims = 8;
+
+hipError_t trace(rt_scene* sc, const rt_settings* s, const ImageParams& im, const Counters& c, hipStream_t st) {
     if (im.max_depth <= 0) return hipSuccess;   // rayColor(ray, depth<=0) is 0: nothing to trace
-    if (precision == RT_PREC_F32) return launch_trace<float>(sc->s32.view, im, c, st);
-    return launch_trace<double>(sc->s64.view, im, c, st);
+    const bool bvh = s->accel == RT_ACCEL_BVH || (s->accel == RT_ACCEL_AUTO && sc->bvh_prims >= kAutoBvhPrims);
+    if (s->precision == RT_PREC_F32) return launch_trace<float>(sc->s32.view, im, c, bvh, st);
+    return launch_trace<double>(sc->s64.view, im, c, bvh, st);
 }
 
 }  // namespace
@@ -221,11 +242,13 @@ int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out) {
     HostScene hs;
     std::string err;
     if (!pack_host(*desc, hs, err)) return fail(RT_ERR_INVALID, "%s", err.c_str());
+    build_bvhs(hs);
     int rc;
     HIP_TRY(hipSetDevice(device));
     rt_scene* sc = new rt_scene();
     sc->device = device;
     sc->num_prims = hs.num_prims;
+    sc->bvh_prims = (int)(hs.sphere_r.size() + hs.tri_mat.size());
     sc->record_bytes = hs.record_bytes;
     if ((rc = build_device(sc->s64, hs, *desc)) || (rc = build_device(sc->s32, hs, *desc))) {
         rt_scene_destroy(sc);
@@ -296,7 +319,7 @@ int rt_render(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progr
         bi.s_begin = b;
         bi.s_end = std::min(s1, b + batch);
         HIP_TRY(hipEventRecord(sc->ev[0], sc->stream));
-        HIP_TRY(trace(sc, s->precision, bi, c, sc->stream));
+        HIP_TRY(trace(sc, s, bi, c, sc->stream));
         HIP_TRY(hipEventRecord(sc->ev[1], sc->stream));
         HIP_TRY(hipEventSynchronize(sc->ev[1]));
         float ms = 0;
@@ -350,7 +373,7 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
     ImageParams im = image_params(s, cw, ch);
     Counters c{d_sum, nullptr, nullptr, sc->total.p};
     HIP_TRY(hipEventRecord(sc->ev[0], st));
-    HIP_TRY(trace(sc, s->precision, im, c, st));
+    HIP_TRY(trace(sc, s, im, c, st));
     HIP_TRY(hipEventRecord(sc->ev[1], st));
     if (sync || stats) {
         unsigned long long total = 0;

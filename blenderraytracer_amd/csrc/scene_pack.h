@@ -4,6 +4,8 @@
 // World.objects insertion order that decides ties (js/world.js:24-30).  A mesh is always its own
 // run: inside it the LAST equal-t triangle wins (geometry.js:253-259).
 #pragma once
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -17,6 +19,10 @@ struct HostScene {   // precision-independent staging, binary64 as packed by the
     std::vector<Run> runs;
     std::vector<double> spheres, sphere_r, planes, boxes, tris;   // 4, 1, 6, 6, 12 doubles per record
     std::vector<int> sphere_mat, plane_mat, box_mat, tri_mat;
+    std::vector<int> sphere_obj, plane_obj, box_obj, tri_obj;     // World.objects index (tie order)
+    std::vector<double> tri_verts;                                // v0, v1, v2 as given (BVH bounds)
+    std::vector<BvhNode> sphere_bvh, tri_bvh;                     // built by build_bvhs()
+    std::vector<int> sphere_bvh_prims, tri_bvh_prims;
     int num_prims = 0;
     double record_bytes = 0;      // SURVEY §8d canonical bytes tested per segment
 };
@@ -43,6 +49,7 @@ inline bool pack_host(const rt_scene_desc& d, HostScene& hs, std::string& err) {
             hs.spheres.insert(hs.spheres.end(), {o.g[0], o.g[1], o.g[2], r * r});
             hs.sphere_r.push_back(r);
             hs.sphere_mat.push_back(o.material);
+            hs.sphere_obj.push_back(i);
             push_run(RUN_SPHERES, k, k + 1, -1);
             hs.num_prims += 1;
             hs.record_bytes += 16;
@@ -52,6 +59,7 @@ inline bool pack_host(const rt_scene_desc& d, HostScene& hs, std::string& err) {
             const int k = (int)hs.plane_mat.size();
             hs.planes.insert(hs.planes.end(), o.g, o.g + 6);
             hs.plane_mat.push_back(o.material);
+            hs.plane_obj.push_back(i);
             push_run(RUN_PLANES, k, k + 1, -1);
             hs.num_prims += 1;
             hs.record_bytes += 24;
@@ -61,6 +69,7 @@ inline bool pack_host(const rt_scene_desc& d, HostScene& hs, std::string& err) {
             const int k = (int)hs.box_mat.size();
             hs.boxes.insert(hs.boxes.end(), o.g, o.g + 6);
             hs.box_mat.push_back(o.material);
+            hs.box_obj.push_back(i);
             push_run(RUN_BOXES, k, k + 1, -1);
             hs.num_prims += 1;
             hs.record_bytes += 24;
@@ -84,6 +93,8 @@ inline bool pack_host(const rt_scene_desc& d, HostScene& hs, std::string& err) {
                 hs.tris.insert(hs.tris.end(), {v[0], v[1], v[2], v[3] - v[0], v[4] - v[1], v[5] - v[2],
                                                v[6] - v[0], v[7] - v[1], v[8] - v[2], v[9], v[10], v[11]});
                 hs.tri_mat.push_back(o.material);
+                hs.tri_obj.push_back(i);
+                hs.tri_verts.insert(hs.tri_verts.end(), v, v + 9);
             }
             push_run(o.type == RT_OBJ_TRIANGLE ? RUN_TRIANGLES : RUN_MESH, k, k + cnt, o.material);
             hs.num_prims += cnt;
@@ -99,6 +110,167 @@ inline bool pack_host(const rt_scene_desc& d, HostScene& hs, std::string& err) {
     return true;
 }
 
+// ---- BVH (binned SAH, preorder with skip links) over spheres and over triangles ---------------------
+// Node bounds are inflated on every axis by 2^-19 max|bound| (the node's largest coordinate) and
+// rounded outward to binary32, so that the binary32 slab test of pt_core.h (bvh_node_hit) is
+// conservative; see bvh_conservative_bound there.
+struct BuildPrim { double lo[3], hi[3], c[3]; int idx; };
+
+inline float round_down_f32(double y) {
+    float f = (float)y;
+    if ((double)f > y) f = std::nextafter(f, -INFINITY);
+    return f;
+}
+inline float round_up_f32(double y) {
+    float f = (float)y;
+    if ((double)f < y) f = std::nextafter(f, INFINITY);
+    return f;
+}
+// a primitive with a NaN coordinate never wins a closest-hit comparison; its bounds become the whole
+// space so that it cannot poison the bounds of the primitives sharing its nodes
+inline void sanitize_prim(BuildPrim& p) {
+    bool bad = false;
+    for (int a = 0; a < 3; ++a) bad |= p.lo[a] != p.lo[a] || p.hi[a] != p.hi[a];
+    if (!bad) return;
+    for (int a = 0; a < 3; ++a) { p.lo[a] = -INFINITY; p.hi[a] = INFINITY; p.c[a] = 0; }
+}
+
+struct BvhBuilder {
+    std::vector<BuildPrim> prims;
+    std::vector<BvhNode> nodes;
+    std::vector<int> order;
+    static constexpr int kLeafMax = 4;
+    static constexpr int kBins = 16;
+
+    static double area(const double* lo, const double* hi) {
+        const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+        return x * y + y * z + z * x;
+    }
+
+    int build(int begin, int end) {
+        const int me = (int)nodes.size();
+        nodes.push_back(BvhNode{});
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int k = begin; k < end; ++k)
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], prims[k].lo[a]);
+                hi[a] = std::max(hi[a], prims[k].hi[a]);
+                clo[a] = std::min(clo[a], prims[k].c[a]);
+                chi[a] = std::max(chi[a], prims[k].c[a]);
+            }
+        BvhNode n{};
+        double m = 0;
+        for (int a = 0; a < 3; ++a) m = std::max(m, std::max(std::fabs(lo[a]), std::fabs(hi[a])));
+        const double pad = m * 0x1p-19 + 0x1p-100;
+        for (int a = 0; a < 3; ++a) {
+            n.lo[a] = round_down_f32(lo[a] - pad);
+            n.hi[a] = round_up_f32(hi[a] + pad);
+        }
+        const int count = end - begin;
+        int axis = 0;
+        for (int a = 1; a < 3; ++a)
+            if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
+        const double extent = chi[axis] - clo[axis];
+        int mid = -1;
+        if (count > kLeafMax && extent > 0) {
+            // binned SAH along the widest centroid axis
+            struct Bin { double lo[3], hi[3]; int n; };
+            Bin bins[kBins];
+            for (auto& b : bins) {
+                b.n = 0;
+                for (int a = 0; a < 3; ++a) { b.lo[a] = INFINITY; b.hi[a] = -INFINITY; }
+            }
+            auto bin_of = [&](const BuildPrim& p) {
+                int b = (int)((p.c[axis] - clo[axis]) / extent * kBins);
+                return std::min(kBins - 1, std::max(0, b));
+            };
+            for (int k = begin; k < end; ++k) {
+                Bin& b = bins[bin_of(prims[k])];
+                b.n++;
+                for (int a = 0; a < 3; ++a) {
+                    b.lo[a] = std::min(b.lo[a], prims[k].lo[a]);
+                    b.hi[a] = std::max(b.hi[a], prims[k].hi[a]);
+                }
+            }
+            double best = INFINITY;
+            int best_split = -1;
+            for (int s = 1; s < kBins; ++s) {
+                double llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                double rlo[3] = {INFINITY, INFINITY, INFINITY}, rhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                int nl = 0, nr = 0;
+                for (int b = 0; b < kBins; ++b) {
+                    double* l = b < s ? llo : rlo;
+                    double* h = b < s ? lhi : rhi;
+                    (b < s ? nl : nr) += bins[b].n;
+                    for (int a = 0; a < 3; ++a) {
+                        l[a] = std::min(l[a], bins[b].lo[a]);
+                        h[a] = std::max(h[a], bins[b].hi[a]);
+                    }
+                }
+                if (!nl || !nr) continue;
+                const double cost = nl * area(llo, lhi) + nr * area(rlo, rhi);
+                if (cost < best) { best = cost; best_split = s; }
+            }
+            if (best_split > 0) {
+                auto it = std::partition(prims.begin() + begin, prims.begin() + end,
+                                         [&](const BuildPrim& p) { return bin_of(p) < best_split; });
+                mid = (int)(it - prims.begin());
+            }
+            if (mid <= begin || mid >= end) {       // degenerate binning: median split
+                mid = (begin + end) / 2;
+                std::nth_element(prims.begin() + begin, prims.begin() + mid, prims.begin() + end,
+                                 [&](const BuildPrim& p, const BuildPrim& q) { return p.c[axis] < q.c[axis]; });
+            }
+        } else if (count > kLeafMax) {              // all centroids equal: split by count
+            mid = (begin + end) / 2;
+        }
+        if (mid < 0) {                              // leaf
+            n.fc = ((int)order.size() << 4) | count;
+            for (int k = begin; k < end; ++k) order.push_back(prims[k].idx);
+        } else {
+            n.fc = 0;
+            build(begin, mid);                      // first child = me + 1 (preorder)
+            build(mid, end);
+        }
+        n.skip = (int)nodes.size();                 // next node after this subtree
+        nodes[me] = n;
+        return me;
+    }
+};
+
+inline void build_bvhs(HostScene& hs) {
+    BvhBuilder sb;
+    for (size_t i = 0; i < hs.sphere_r.size(); ++i) {
+        const double* s = &hs.spheres[4 * i];
+        const double r = std::fabs(hs.sphere_r[i]);       // negative radius: same sphere, inverted normal
+        BuildPrim p;
+        for (int a = 0; a < 3; ++a) { p.lo[a] = s[a] - r; p.hi[a] = s[a] + r; p.c[a] = s[a]; }
+        p.idx = (int)i;
+        sanitize_prim(p);
+        sb.prims.push_back(p);
+    }
+    if (!sb.prims.empty()) sb.build(0, (int)sb.prims.size());
+    hs.sphere_bvh = std::move(sb.nodes);
+    hs.sphere_bvh_prims = std::move(sb.order);
+    BvhBuilder tb;
+    for (size_t i = 0; i < hs.tri_mat.size(); ++i) {
+        const double* v = &hs.tri_verts[9 * i];
+        BuildPrim p;
+        for (int a = 0; a < 3; ++a) {
+            p.lo[a] = std::min(v[a], std::min(v[3 + a], v[6 + a]));
+            p.hi[a] = std::max(v[a], std::max(v[3 + a], v[6 + a]));
+            p.c[a] = (p.lo[a] + p.hi[a]) * 0.5;
+        }
+        p.idx = (int)i;
+        sanitize_prim(p);
+        tb.prims.push_back(p);
+    }
+    if (!tb.prims.empty()) tb.build(0, (int)tb.prims.size());
+    hs.tri_bvh = std::move(tb.nodes);
+    hs.tri_bvh_prims = std::move(tb.order);
+}
+
 // Record arrays of one precision (host memory); rt_capi.cpp uploads them, tests/hostcheck uses them.
 template <class R>
 struct HostRecords {
@@ -110,6 +282,11 @@ struct HostRecords {
     std::vector<TriRec<R>> tris;
     std::vector<MatRec<R>> mats;
     std::vector<int> perm;
+    // BVH leaf order copies (bvh_spheres[k] = spheres[bvh_sphere_key[k].id], same for triangles)
+    std::vector<SphereRec<R>> bvh_spheres;
+    std::vector<SphereFilter> bvh_sphere_filter;
+    std::vector<PrimKey> bvh_sphere_key, bvh_tri_key;
+    std::vector<TriRec<R>> bvh_tris;
 };
 
 template <class R>
@@ -159,6 +336,15 @@ void make_records(const HostScene& hs, const rt_scene_desc& d, HostRecords<R>& o
         out.mats[i] = r;
     }
     out.perm.assign(d.perm, d.perm + 512);
+    for (int id : hs.sphere_bvh_prims) {
+        out.bvh_spheres.push_back(out.spheres[id]);
+        out.bvh_sphere_filter.push_back(out.sphere_filter[id]);
+        out.bvh_sphere_key.push_back(PrimKey{id, hs.sphere_obj[id]});
+    }
+    for (int id : hs.tri_bvh_prims) {
+        out.bvh_tris.push_back(out.tris[id]);
+        out.bvh_tri_key.push_back(PrimKey{id, hs.tri_obj[id]});
+    }
 }
 
 // Camera / background constants of the SceneView (pointers are set by the caller).
@@ -167,6 +353,10 @@ void fill_view_constants(SceneView<R>& v, const HostScene& hs, const rt_scene_de
     v.num_runs = (int)hs.runs.size();
     v.num_spheres = (int)hs.sphere_r.size();
     v.num_prims = hs.num_prims;
+    v.num_planes = (int)hs.plane_mat.size();
+    v.num_boxes = (int)hs.box_mat.size();
+    v.num_sphere_nodes = (int)hs.sphere_bvh.size();
+    v.num_tri_nodes = (int)hs.tri_bvh.size();
     const rt_camera_desc& c = d.camera;
     for (int k = 0; k < 3; ++k) {
         v.cam_o[k] = (R)c.origin[k];

@@ -30,6 +30,7 @@ export function loadNative() {
 export const AA = { supersampling: 0, stochastic: 1 };            // anything else: pixel centre (2)
 export const TONE = { aces: 1, linear: 2 };                        // anything else: reinhard (0)
 export const PRECISION = { f64: 0, f32: 1 };
+export const ACCEL = { auto: 0, brute: 1, bvh: 2 };
 
 // rt_settings from RayTracer fields (ray-tracer.js:23-33, :201, :125-161)
 export function settingsOf(rt, opts = {}) {
@@ -43,6 +44,7 @@ export function settingsOf(rt, opts = {}) {
         seed: (opts.seed || 0) >>> 0,
         precision: PRECISION[opts.precision || 'f64'],
         batchSamples: opts.batchSamples || 0,
+        accel: ACCEL[opts.accel || 'auto'],
         cropX0: opts.crop ? opts.crop[0] : 0, cropY0: opts.crop ? opts.crop[1] : 0,
         cropW: opts.crop ? opts.crop[2] : 0, cropH: opts.crop ? opts.crop[3] : 0,
         wantMean: opts.wantMean ? 1 : 0, wantCounts: opts.wantCounts ? 1 : 0,

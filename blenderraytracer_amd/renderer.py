@@ -17,7 +17,7 @@ from .scene import PackedScene, default_scene, load_from_json, setup_camera, key
 
 def settings_struct(width, height, samples, max_bounces, anti_aliasing, tone_mapping, exposure, gamma, seed,
                     crop=None, precision=capi.RT_PREC_F64, sample_range=None, batch_samples=0, denoising=False,
-                    denoise_strength=0.5):
+                    denoise_strength=0.5, accel=capi.RT_ACCEL_AUTO):
     """rt_settings from RayTracer fields, resolving sampleCount (ray-tracer.js:201) and the string
     switches of getAntiAliasSample (:125-149) and toneMap (:151-161)."""
     s = capi.Settings()
@@ -35,6 +35,7 @@ def settings_struct(width, height, samples, max_bounces, anti_aliasing, tone_map
         s.crop_x0, s.crop_y0, s.crop_w, s.crop_h = (int(v) for v in crop)
     s.precision = int(precision)
     s.batch_samples = int(batch_samples)
+    s.accel = int(accel)
     if truthy(denoising):
         # post-processor.js:55: Math.exp(-(kx*kx + ky*ky) / (2 * strength * strength)) for kx^2+ky^2 = 1, 2
         st = float(denoise_strength)
@@ -44,11 +45,12 @@ def settings_struct(width, height, samples, max_bounces, anti_aliasing, tone_map
 
 
 class GpuRayTracer:
-    def __init__(self, width, height, seed=0, device=0, precision=capi.RT_PREC_F64):
+    def __init__(self, width, height, seed=0, device=0, precision=capi.RT_PREC_F64, accel=capi.RT_ACCEL_AUTO):
         self.width, self.height = int(width), int(height)
         self.seed = seed
         self.device = device
         self.precision = precision
+        self.accel = accel
         self.max_bounces, self.samples, self.gamma, self.exposure = 5, 4, 2.2, 1.0
         self.tone_mapping, self.anti_aliasing = "reinhard", "supersampling"
         self.denoising, self.denoise_strength = False, 0.5
@@ -109,7 +111,7 @@ class GpuRayTracer:
         return settings_struct(self.width, self.height, self.samples, self.max_bounces, self.anti_aliasing,
                                self.tone_mapping, self.exposure, self.gamma, self.seed, crop=crop,
                                precision=self.precision, sample_range=sample_range, batch_samples=batch_samples,
-                               denoising=self.denoising, denoise_strength=self.denoise_strength)
+                               denoising=self.denoising, denoise_strength=self.denoise_strength, accel=self.accel)
 
     def scene_handle(self):
         lib = capi.load_library()

@@ -74,6 +74,11 @@ typedef enum rt_tone_map { RT_TM_REINHARD = 0, RT_TM_ACES = 1, RT_TM_LINEAR = 2 
  * F32 is the fast mode; its per-channel RMS vs the reference is measured in tests. */
 typedef enum rt_precision { RT_PREC_F64 = 0, RT_PREC_F32 = 1 } rt_precision;
 
+/* World.hit evaluation.  BRUTE walks World.objects in order (world.js:24-30); BVH walks one bounding
+ * volume hierarchy over the spheres and one over the triangles (built by rt_scene_create) with the
+ * same tie-breaking, so both give bit-identical renders.  AUTO picks BVH for large scenes. */
+typedef enum rt_accel { RT_ACCEL_AUTO = 0, RT_ACCEL_BRUTE = 1, RT_ACCEL_BVH = 2 } rt_accel;
+
 typedef struct rt_material_desc {
     int32_t type;          /* rt_material_type */
     int32_t _pad;
@@ -139,6 +144,8 @@ typedef struct rt_settings {
                                   needs the full frame (crop_w/h = 0 or the whole image) */
     double denoise_weights[2]; /* Math.exp(-1/(2s*s)), Math.exp(-2/(2s*s)), s = denoiseStrength, evaluated by
                                   the host with its own exp (post-processor.js:55) */
+    int32_t accel;             /* rt_accel: how World.hit is evaluated (results are identical) */
+    int32_t _pad;
 } rt_settings;
 
 /* Host outputs of rt_render, each optional (NULL = not wanted). n = crop_w*crop_h pixels,

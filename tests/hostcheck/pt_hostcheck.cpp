@@ -9,20 +9,36 @@
 
 using namespace rt;
 
+// host-side scene staging exactly as rt_scene_create builds it (pack_host, build_bvhs, make_records)
+template <class R>
+struct HostView {
+    HostScene hs;
+    HostRecords<R> rec;
+    SceneView<R> v{};
+    bool init(const rt_scene_desc* d) {
+        std::string err;
+        if (!pack_host(*d, hs, err)) return false;
+        build_bvhs(hs);
+        make_records(hs, *d, rec);
+        v.runs = hs.runs.data();
+        v.spheres = rec.spheres.data(); v.sphere_filter = rec.sphere_filter.data(); v.sphere_r = rec.sphere_r.data(); v.planes = rec.planes.data();
+        v.boxes = rec.boxes.data(); v.tris = rec.tris.data(); v.sphere_mat = hs.sphere_mat.data();
+        v.plane_mat = hs.plane_mat.data(); v.box_mat = hs.box_mat.data(); v.tri_mat = hs.tri_mat.data();
+        v.mats = rec.mats.data(); v.perm = rec.perm.data();
+        v.plane_obj = hs.plane_obj.data(); v.box_obj = hs.box_obj.data();
+        v.sphere_nodes = hs.sphere_bvh.data(); v.tri_nodes = hs.tri_bvh.data();
+        v.bvh_spheres = rec.bvh_spheres.data(); v.bvh_sphere_filter = rec.bvh_sphere_filter.data();
+        v.bvh_sphere_key = rec.bvh_sphere_key.data(); v.bvh_tris = rec.bvh_tris.data(); v.bvh_tri_key = rec.bvh_tri_key.data();
+        fill_view_constants(v, hs, *d);
+        return true;
+    }
+};
+
 template <class R>
 static int render(const rt_scene_desc* d, const rt_settings* s, double* sum, uint32_t* segs, uint32_t* draws) {
-    HostScene hs;
-    std::string err;
-    if (!pack_host(*d, hs, err)) return -1;
-    HostRecords<R> rec;
-    make_records(hs, *d, rec);
-    SceneView<R> v{};
-    v.runs = hs.runs.data();
-    v.spheres = rec.spheres.data(); v.sphere_filter = rec.sphere_filter.data(); v.sphere_r = rec.sphere_r.data(); v.planes = rec.planes.data();
-    v.boxes = rec.boxes.data(); v.tris = rec.tris.data(); v.sphere_mat = hs.sphere_mat.data();
-    v.plane_mat = hs.plane_mat.data(); v.box_mat = hs.box_mat.data(); v.tri_mat = hs.tri_mat.data();
-    v.mats = rec.mats.data(); v.perm = rec.perm.data();
-    fill_view_constants(v, hs, *d);
+    HostView<R> hv;
+    if (!hv.init(d)) return -1;
+    const SceneView<R>& v = hv.v;
     ImageParams im{};
     im.width = s->width; im.height = s->height;
     im.x0 = s->crop_x0; im.y0 = s->crop_y0;
@@ -38,7 +54,9 @@ static int render(const rt_scene_desc* d, const rt_settings* s, double* sum, uin
         for (int cx = 0; cx < im.cw; ++cx) {
             const size_t q = (size_t)cy * im.cw + cx;
             PixelResult r{0, 0};
-            if (im.max_depth > 0) r = trace_pixel<R, true>(v, im, cx, cy, im.s_end, sum + 3 * q);
+            if (im.max_depth > 0)
+                r = s->accel == RT_ACCEL_BVH ? trace_pixel<R, true, ACC_BVH>(v, im, cx, cy, im.s_end, sum + 3 * q)
+                                             : trace_pixel<R, true, ACC_BRUTE>(v, im, cx, cy, im.s_end, sum + 3 * q);
             segs[q] = r.segments;
             draws[q] = r.draws;
         }
@@ -54,6 +72,7 @@ extern "C" int ptc_render(const rt_scene_desc* d, const rt_settings* s, double* 
 // Returns the number of spheres the filter rejected although disc64 >= 0 (must be 0); writes the
 // largest |disc32 - disc64| / (A Q) seen and the fraction of sure misses the filter rejects.
 #include <cmath>
+#include <cstring>
 #include <random>
 extern "C" int ptc_sphere_filter_check(long long n, unsigned seed, double* max_ratio, double* reject_frac) {
     std::mt19937_64 gen(seed);
@@ -104,4 +123,62 @@ extern "C" int ptc_sphere_filter_check(long long n, unsigned seed, double* max_r
     *max_ratio = worst;
     *reject_frac = misses ? (double)rejected / misses : 0;
     return (int)violations;
+}
+
+// BVH stress: n random rays per scene, closest_hit (World order) vs closest_hit_bvh.  Rays start at
+// random points and aim at random primitives' surfaces (near-tangent for spheres, near edges and
+// vertices for triangles) to exercise the conservative node bounds.  Returns the number of rays
+// whose (t, primitive kind, index) differ.
+extern "C" long long ptc_bvh_check(const rt_scene_desc* d, long long n, unsigned seed, long long* hits) {
+    HostView<double> hv;
+    if (!hv.init(d)) return -1;
+    const SceneView<double>& v = hv.v;
+    std::mt19937_64 gen(seed);
+    std::uniform_real_distribution<double> U(-1.0, 1.0);
+    const HostScene& hs = hv.hs;
+    const int ns = (int)hs.sphere_r.size(), nt = (int)hs.tri_mat.size();
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    for (int i = 0; i < ns; ++i)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], hs.spheres[4 * i + a] - std::fabs(hs.sphere_r[i]));
+            hi[a] = std::max(hi[a], hs.spheres[4 * i + a] + std::fabs(hs.sphere_r[i]));
+        }
+    for (int i = 0; i < 3 * nt; ++i)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], hs.tri_verts[3 * i + a]);
+            hi[a] = std::max(hi[a], hs.tri_verts[3 * i + a]);
+        }
+    long long bad = 0, nh = 0;
+    for (long long it = 0; it < n; ++it) {
+        double o[3], target[3];
+        for (int a = 0; a < 3; ++a) o[a] = lo[a] + (hi[a] - lo[a]) * (0.5 + 0.75 * U(gen));
+        const int pick = (int)(std::fabs(U(gen)) * (ns + nt));
+        const double eps = std::pow(10.0, -10.0 * std::fabs(U(gen)) - 2.0) * (U(gen) < 0 ? -1 : 1);
+        if (pick < ns) {                   // a point at distance r (1 + eps) from the centre, off the ray
+            const double* c = &hs.spheres[4 * pick];
+            double w[3] = {U(gen), U(gen), U(gen)};
+            const double wn = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+            for (int a = 0; a < 3; ++a) target[a] = c[a] + w[a] / wn * std::fabs(hs.sphere_r[pick]) * (1 + eps);
+        } else if (nt > 0) {               // a point on or just off an edge / vertex of a triangle
+            const double* t = &hs.tri_verts[9 * std::min(pick - ns, nt - 1)];
+            double u = std::fabs(U(gen)), w = std::fabs(U(gen));
+            const int mode = (int)(std::fabs(U(gen)) * 3);
+            if (mode == 0) w = 0;                        // edge v0-v1
+            else if (mode == 1) { u = 1 + eps; w = 0; }  // past vertex v1
+            else { w = 1 - u + eps; }                     // edge v1-v2
+            for (int a = 0; a < 3; ++a) target[a] = t[a] + u * (t[3 + a] - t[a]) + w * (t[6 + a] - t[a]);
+        } else {
+            continue;
+        }
+        const double dl = std::pow(10.0, 2.0 * U(gen));
+        V3<double> O{o[0], o[1], o[2]}, D{(target[0] - o[0]) * dl, (target[1] - o[1]) * dl, (target[2] - o[2]) * dl};
+        const Closest<double> a = closest_hit<double, false>(v, O, D);
+        const Closest<double> b = closest_hit_bvh(v, O, D);
+        if (a.kind != HIT_NONE) ++nh;
+        const bool same = a.kind == b.kind && (a.kind == HIT_NONE || (a.idx == b.idx && a.mat == b.mat &&
+                                                                     std::memcmp(&a.t, &b.t, 8) == 0));
+        bad += !same;
+    }
+    if (hits) *hits = nh;
+    return bad;
 }

@@ -32,7 +32,17 @@ def lib():
         _lib = C.CDLL(build())
         _lib.ptc_render.argtypes = [C.POINTER(capi.SceneDesc), C.POINTER(capi.Settings), C.POINTER(C.c_double),
                                     C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        _lib.ptc_bvh_check.argtypes = [C.POINTER(capi.SceneDesc), C.c_longlong, C.c_uint, C.POINTER(C.c_longlong)]
+        _lib.ptc_bvh_check.restype = C.c_longlong
     return _lib
+
+
+def bvh_check(packed, n, seed):
+    """(rays whose brute-force and BVH closest hits differ, rays that hit something)"""
+    hits = C.c_longlong()
+    bad = lib().ptc_bvh_check(C.byref(packed.desc), n, seed, C.byref(hits))
+    assert bad >= 0
+    return bad, hits.value
 
 
 def render(packed, settings):
