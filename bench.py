@@ -125,13 +125,14 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    kernel_ms, segs, abytes = [], [], []
+    kernel_ms, segs, abytes, work = [], [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         job.step()
         kernel_ms.append(job.stats.kernel_ms)
         segs.append(job.stats.segments)
         abytes.append(job.stats.algorithmic_bytes)
+        work.append((job.stats.node_visits, job.stats.sphere_tests, job.stats.tri_tests))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -148,7 +149,13 @@ def main():
         a_bytes = sum(abytes) / len(abytes)
         achieved = a_bytes / (k_ms * 1e-3) / 1e9
         seg_launch = sum(segs) / len(segs)
-        flops = seg_launch * flops_per_segment
+        nodes, sph, tri = (sum(w[k] for w in work) / len(work) for k in range(3))
+        bvh = nodes > 0
+        if bvh:   # BVH: slab test 12 flops/node + per-test flops of the leaves + brute planes/boxes
+            brute = sum(FLOPS[k] for k in packed.kinds if k in ("plane", "box"))
+            flops = 12 * nodes + FLOPS["sphere"] * sph + FLOPS["triangle"] * tri + seg_launch * brute
+        else:
+            flops = seg_launch * flops_per_segment
         rank_samples = cfg["w"] * cfg["h"] * (job.range[1] - job.range[0])
         traffic = load_traffic(args.config, args.precision)
         line = {
@@ -165,11 +172,15 @@ def main():
                          "traffic": traffic,
                          "kernel": "trace_kernel", "kernel_ms": round(k_ms, 3),
                          "algorithmic_bytes_per_launch": a_bytes,
-                         "definition": "segments x sum(prim record bytes: sphere 16, plane 24, box 24, tri 36) "
-                                       "+ 12 B/pixel (SURVEY 8d); served from SGPR/L1, not HBM"},
+                         "definition": ("BVH: 64 B/node visited + 16 B/sphere + 36 B/triangle tested + segments x "
+                                        "24 B/plane|box + 12 B/pixel" if bvh else
+                                        "segments x sum(prim record bytes: sphere 16, plane 24, box 24, tri 36) "
+                                        "+ 12 B/pixel (SURVEY 8d); served from SGPR/L1, not HBM"),
+                         "bvh_nodes_per_segment": round(nodes / seg_launch, 3) if bvh else None,
+                         "prim_tests_per_segment": round((sph + tri) / seg_launch, 3) if bvh else None},
             "valu": {"achieved": round(flops / (k_ms * 1e-3) / 1e12, 3), "peak": VALU_PEAK_TFLOPS[args.precision],
                      "unit": "TFLOP/s", "frac": round(flops / (k_ms * 1e-3) / 1e12 / VALU_PEAK_TFLOPS[args.precision], 4),
-                     "flops_per_segment": flops_per_segment},
+                     "flops_per_segment": round(flops / seg_launch, 2)},
             "segments_per_sample": round(seg_launch / rank_samples, 4),
             "kernel_msamples_per_s": round(rank_samples / (k_ms * 1e-3) / 1e6, 3),
             "cpu_baseline": cpu,

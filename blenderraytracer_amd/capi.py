@@ -66,7 +66,8 @@ class Output(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("kernel_ms", C.c_double), ("finalize_ms", C.c_double), ("wall_ms", C.c_double),
                 ("samples", C.c_uint64), ("segments", C.c_uint64), ("prim_tests", C.c_uint64),
-                ("algorithmic_bytes", C.c_double)]
+                ("algorithmic_bytes", C.c_double), ("node_visits", C.c_uint64),
+                ("sphere_tests", C.c_uint64), ("tri_tests", C.c_uint64)]
 
 
 PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.c_double, C.c_void_p)

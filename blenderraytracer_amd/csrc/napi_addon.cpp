@@ -250,7 +250,8 @@ void complete(napi_env env, napi_status, void* data) {
         const struct { const char* k; double v; } fields[] = {
             {"kernelMs", job->stats.kernel_ms}, {"finalizeMs", job->stats.finalize_ms}, {"wallMs", job->stats.wall_ms},
             {"samples", (double)job->stats.samples}, {"segments", (double)job->stats.segments},
-            {"primTests", (double)job->stats.prim_tests}, {"algorithmicBytes", job->stats.algorithmic_bytes}};
+            {"primTests", (double)job->stats.prim_tests}, {"algorithmicBytes", job->stats.algorithmic_bytes},
+            {"nodeVisits", (double)job->stats.node_visits}};
         for (const auto& f : fields) {
             napi_create_double(env, f.v, &v);
             napi_set_named_property(env, stats, f.k, v);

@@ -80,6 +80,12 @@ template <class R> struct MatRec { int type, pad; R albedo[3]; R rough; R ior; R
 // primitives at leaf-order positions [first, first+count), 0 for an internal node.
 struct BvhNode { float lo[3]; int skip; float hi[3]; int fc; };
 struct PrimKey { int id, obj; };   // index into the World-order arrays, World.objects index
+// The same tree as 64-B two-child nodes for the ordered stack walk: box k = {lo, hi} of child k,
+// child[k] >= 0 an inner node, < 0 the leaf ~fc.  Depth <= RT_BVH_STACK (scene_pack.h).
+struct Bvh2Node { float box[2][6]; int child[2]; int pad[2]; };
+#ifndef RT_BVH_STACK
+#define RT_BVH_STACK 32
+#endif
 
 template <class R>
 struct SceneView {
@@ -113,6 +119,8 @@ struct SceneView {
     int num_tri_nodes;
     const TriRec<R>* bvh_tris;
     const PrimKey* bvh_tri_key;
+    const Bvh2Node* sphere_wide;   // null when there are no spheres
+    const Bvh2Node* tri_wide;      // null when there are no triangles
     // camera (camera.js:8-36 vectors, computed on the host in binary64)
     R cam_o[3], cam_llc[3], cam_h[3], cam_v[3], cam_u[3], cam_vv[3], cam_w[3];
     R lens_radius;
@@ -365,8 +373,77 @@ RT_HD bool bvh_node_hit(const BvhNode& n, const BvhRay& r, float tlimit) {
 // Closest hit through the BVHs: planes and boxes (usually few, often large) brute force first, then
 // the sphere BVH and the triangle BVH, each a stackless walk of the preorder node array.  Lanes walk
 // their own paths (per-lane node loads); leaf records are contiguous in leaf order.
-template <class R>
-RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d) {
+struct Work { uint32_t nodes, spheres, tris; };   // BVH nodes visited, sphere / triangle tests (stats)
+#ifndef RT_BVH_COUNT
+#define RT_BVH_COUNT 1
+#endif
+#if RT_BVH_COUNT
+#define RT_COUNT(x) (x)
+#else
+#define RT_COUNT(x) ((void)0)
+#endif
+
+// per-lane traversal stack of the ordered walk: entry k of this lane at base[k * stride] (LDS on the
+// GPU, strided by the workgroup size so a wave's accesses are conflict-free)
+struct BvhStack { int* base; int stride; };
+
+RT_HD bool bvh_box_hit(const float* bx, const BvhRay& r, float tlimit, float& tn) {
+    const float x0 = (bx[0] - r.olo[0]) * r.inv[0], x1 = (bx[3] - r.ohi[0]) * r.inv[0];
+    const float y0 = (bx[1] - r.olo[1]) * r.inv[1], y1 = (bx[4] - r.ohi[1]) * r.inv[1];
+    const float z0 = (bx[2] - r.olo[2]) * r.inv[2], z1 = (bx[5] - r.ohi[2]) * r.inv[2];
+    tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.0f));
+    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tlimit));
+    return tn <= tf;
+}
+
+// Walk one BVH and call leaf(fc) for every leaf whose box the ray reaches before the current best.
+// WIDE: ordered walk over Bvh2Node (both child boxes per 64-B node, nearer child first, the other
+// pushed on the lane's stack); otherwise the stackless preorder walk over BvhNode skip links.
+template <bool WIDE, class Leaf>
+RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const BvhRay& br, const float& tl,
+                    BvhStack stk, Work& w, Leaf&& leaf) {
+    if constexpr (WIDE) {
+        int sp = 0, cur = 0;
+        for (;;) {
+            if (cur >= 0) {
+                const Bvh2Node n = wide[cur];
+                RT_COUNT(++w.nodes);
+                float t0, t1;
+                const bool h0 = bvh_box_hit(n.box[0], br, tl, t0), h1 = bvh_box_hit(n.box[1], br, tl, t1);
+                if (h0 && h1) {
+                    const bool swap = t1 < t0;
+                    stk.base[(sp++) * stk.stride] = swap ? n.child[0] : n.child[1];
+                    cur = swap ? n.child[1] : n.child[0];
+                    continue;
+                }
+                if (h0 | h1) {
+                    cur = h0 ? n.child[0] : n.child[1];
+                    continue;
+                }
+            } else {
+                leaf(~cur);
+            }
+            if (sp == 0) break;
+            cur = stk.base[(--sp) * stk.stride];
+        }
+    } else {
+        int ni = 0;
+        while (ni < count) {
+            const BvhNode n = nodes[ni];
+            RT_COUNT(++w.nodes);
+            if (!bvh_node_hit(n, br, tl)) { ni = n.skip; continue; }
+            if (n.fc == 0) { ++ni; continue; }
+            ni = n.skip;
+            leaf(n.fc);
+        }
+    }
+}
+
+// Closest hit through the BVHs: planes and boxes (usually few, often large) brute force first, then
+// the sphere BVH and the triangle BVH.  Lanes walk their own paths (per-lane node loads); leaf
+// records are contiguous in leaf order.
+template <class R, bool WIDE>
+RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
     const R tmin = (R)0.001;
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
     for (int i = 0; i < sc.num_planes; ++i) {                                 // geometry.js:56-74
@@ -403,12 +480,9 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d) {
         const R a = dot(d, d);
         FilterRay fr{};
         if constexpr (sizeof(R) == 8) fr = make_filter_ray(o, d);
-        int ni = 0;
-        while (ni < sc.num_sphere_nodes) {
-            const BvhNode n = sc.sphere_nodes[ni];
-            if (!bvh_node_hit(n, br, tl)) { ni = n.skip; continue; }
-            if (n.fc == 0) { ++ni; continue; }
-            const int first = n.fc >> 4, end = first + (n.fc & 15);
+        bvh_walk<WIDE>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w, [&](int fc) {
+            const int first = fc >> 4, end = first + (fc & 15);
+            RT_COUNT(w.spheres += end - first);
             for (int k = first; k < end; ++k) {
                 if constexpr (sizeof(R) == 8)
                     if (!sphere_filter_pass(sc.bvh_sphere_filter[k], fr)) continue;
@@ -420,16 +494,12 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d) {
                     tl = bvh_tlimit(b.t);
                 }
             }
-            ni = n.skip;
-        }
+        });
     }
     if (sc.num_tri_nodes > 0) {
-        int ni = 0;
-        while (ni < sc.num_tri_nodes) {
-            const BvhNode n = sc.tri_nodes[ni];
-            if (!bvh_node_hit(n, br, tl)) { ni = n.skip; continue; }
-            if (n.fc == 0) { ++ni; continue; }
-            const int first = n.fc >> 4, end = first + (n.fc & 15);
+        bvh_walk<WIDE>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, [&](int fc) {
+            const int first = fc >> 4, end = first + (fc & 15);
+            RT_COUNT(w.tris += end - first);
             for (int k = first; k < end; ++k) {
                 R t;
                 if (!triangle_candidate(sc.bvh_tris[k], o, d, tmin, t)) continue;
@@ -439,18 +509,19 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d) {
                     tl = bvh_tlimit(b.t);
                 }
             }
-            ni = n.skip;
-        }
+        });
     }
     return b;
 }
 
 // acceleration modes of the trace kernel
-enum Accel : int { ACC_BRUTE = 0, ACC_LDS = 1, ACC_BVH = 2 };
+enum Accel : int { ACC_BRUTE = 0, ACC_LDS = 1, ACC_BVH = 2, ACC_BVH_STACK = 3 };
 
 template <class R, int ACC>
-RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, const LdsSpheres lds) {
-    if constexpr (ACC == ACC_BVH) return closest_hit_bvh(sc, o, d);
+RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, const LdsSpheres lds, Work& w,
+                                 BvhStack stk) {
+    if constexpr (ACC == ACC_BVH) return closest_hit_bvh<R, false>(sc, o, d, w, stk);
+    else if constexpr (ACC == ACC_BVH_STACK) return closest_hit_bvh<R, true>(sc, o, d, w, stk);
     else return closest_hit<R, ACC == ACC_LDS>(sc, o, d, lds);
 }
 

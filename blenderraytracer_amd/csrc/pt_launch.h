@@ -11,7 +11,7 @@ struct Counters {
     double* sum;               // n*3 running per-pixel radiance sums (read-modify-write)
     uint32_t* segs;            // optional n per-pixel world.hit counts
     uint32_t* draws;           // optional n per-pixel RNG draws
-    unsigned long long* total_segs;   // optional global segment counter
+    unsigned long long* totals;   // optional [segments, BVH nodes, sphere tests, triangle tests]
 };
 
 template <class R>

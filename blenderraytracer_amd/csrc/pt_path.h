@@ -94,15 +94,15 @@ RT_HD bool scatter(const MatRec<R>& m, const Hit<R>& h, V3<R> d, Rng<R>& g, V3<R
     return true;
 }
 
-struct PixelResult { uint32_t segments, draws; };
+struct PixelResult { uint32_t segments, draws; Work work; };
 
 // Trace samples [im.s_begin, s_end) of crop pixel (cx, cy), adding radiance into sum[0..2].
 template <class R, bool COUNT, int ACC = ACC_BRUTE>
 RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int cx, int cy, int s_end, double* sum,
-                              const LdsSpheres lds = LdsSpheres{nullptr}) {
+                              const LdsSpheres lds = LdsSpheres{nullptr}, BvhStack stk = BvhStack{nullptr, 0}) {
     const int i = im.x0 + cx, row = im.y0 + cy, j = im.height - 1 - row;
     const uint32_t pkey = pixel_key(im.seedm, (uint32_t)row * (uint32_t)im.width + (uint32_t)i);
-    PixelResult res{0, 0};
+    PixelResult res{0, 0, {0, 0, 0}};
     int s = im.s_begin;
     double sx = sum[0], sy = sum[1], sz = sum[2];
     Rng<R> g;
@@ -110,7 +110,7 @@ RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int
     int depth = im.max_depth;
     if (s < s_end) start_sample(sc, im, i, j, pkey, s, g, o, d);
     while (s < s_end) {
-        const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, lds);
+        const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, lds, res.work, stk);
         ++res.segments;
         bool done = true;
         V3<R> L = mk<R>(0, 0, 0);

@@ -27,10 +27,16 @@ struct TraceArgs {
 #endif
 
 template <class R, bool COUNT, int ACC>
-__global__ __launch_bounds__(256, ACC == ACC_BVH ? RT_BVH_WAVES_PER_SIMD : RT_MIN_WAVES_PER_SIMD)
+__global__ __launch_bounds__(256, ACC >= ACC_BVH ? RT_BVH_WAVES_PER_SIMD : RT_MIN_WAVES_PER_SIMD)
 void trace_kernel(const TraceArgs<R> args) {
     const ImageParams& im = args.im;
     LdsSpheres lds{nullptr};
+    BvhStack stk{nullptr, 0};
+    if constexpr (ACC == ACC_BVH_STACK) {
+        // per-lane traversal stacks, entry k of thread t at [k * 256 + t] (32 KB per workgroup)
+        __shared__ int bvh_stack[RT_BVH_STACK * 256];
+        stk = BvhStack{bvh_stack + threadIdx.x, 256};
+    }
     if constexpr (ACC == ACC_LDS) {
         // stage the binary32 sphere filter records of the whole scene in LDS (one copy per workgroup)
         extern __shared__ SphereFilter lds_spheres[];
@@ -48,7 +54,7 @@ void trace_kernel(const TraceArgs<R> args) {
     double acc[3] = {0, 0, 0};
     if (valid) { acc[0] = args.c.sum[3 * q]; acc[1] = args.c.sum[3 * q + 1]; acc[2] = args.c.sum[3 * q + 2]; }
     // invalid lanes trace nothing but stay for the wave reduction below
-    const PixelResult r = trace_pixel<R, COUNT, ACC>(args.sc, im, cx, cy, valid ? im.s_end : im.s_begin, acc, lds);
+    const PixelResult r = trace_pixel<R, COUNT, ACC>(args.sc, im, cx, cy, valid ? im.s_end : im.s_begin, acc, lds, stk);
     if (valid) {
         args.c.sum[3 * q] = acc[0]; args.c.sum[3 * q + 1] = acc[1]; args.c.sum[3 * q + 2] = acc[2];
         if (COUNT) {
@@ -56,10 +62,13 @@ void trace_kernel(const TraceArgs<R> args) {
             if (args.c.draws) args.c.draws[q] += r.draws;
         }
     }
-    if (args.c.total_segs) {
-        unsigned long long v = r.segments;
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (lane == 0) atomicAdd(args.c.total_segs, v);
+    if (args.c.totals) {
+        const uint32_t parts[4] = {r.segments, r.work.nodes, r.work.spheres, r.work.tris};
+        for (int k = 0; k < (ACC >= ACC_BVH ? 4 : 1); ++k) {
+            unsigned long long v = parts[k];
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if (lane == 0) atomicAdd(args.c.totals + k, v);
+        }
     }
 }
 
@@ -72,6 +81,16 @@ static int sphere_path_override() {
         v = !e ? -1 : (e[0] == 'l' ? 1 : 0);
     }
     return v;
+}
+
+// RT_BVH_WALK=skip selects the stackless preorder walk instead of the ordered stack walk (A/B runs)
+static bool bvh_stackless() {
+    static int v = -1;
+    if (v == -1) {
+        const char* e = getenv("RT_BVH_WALK");
+        v = e && e[0] == 's' && e[1] == 'k';
+    }
+    return v == 1;
 }
 
 template <class R, int ACC>
@@ -88,7 +107,8 @@ hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Cou
     TraceArgs<R> a{sc, im, c};
     const bool count = c.segs || c.draws;
     if (bvh) {
-        launch_acc<R, ACC_BVH>(a, tiles, 0, count, stream);
+        if (bvh_stackless()) launch_acc<R, ACC_BVH>(a, tiles, 0, count, stream);
+        else launch_acc<R, ACC_BVH_STACK>(a, tiles, 0, count, stream);
         return hipGetLastError();
     }
     const size_t lds_bytes = (size_t)sc.num_spheres * sizeof(SphereFilter);

@@ -89,12 +89,14 @@ struct DeviceScene {
     DevBuf<SphereFilter> bvh_sphere_filter;
     DevBuf<PrimKey> bvh_sphere_key, bvh_tri_key;
     DevBuf<TriRec<R>> bvh_tris;
+    DevBuf<Bvh2Node> sphere_wide, tri_wide;
     SceneView<R> view{};
     void release() {
         runs.release(); spheres.release(); sphere_filter.release(); sphere_r.release(); planes.release(); boxes.release(); tris.release();
         sphere_mat.release(); plane_mat.release(); box_mat.release(); tri_mat.release(); perm.release(); mats.release();
         plane_obj.release(); box_obj.release(); sphere_nodes.release(); tri_nodes.release(); bvh_spheres.release();
         bvh_sphere_filter.release(); bvh_sphere_key.release(); bvh_tri_key.release(); bvh_tris.release();
+        sphere_wide.release(); tri_wide.release();
     }
 };
 
@@ -109,7 +111,7 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     UP(box_mat, hs.box_mat); UP(tri_mat, hs.tri_mat); UP(perm, rec.perm); UP(mats, rec.mats);
     UP(plane_obj, hs.plane_obj); UP(box_obj, hs.box_obj); UP(sphere_nodes, hs.sphere_bvh); UP(tri_nodes, hs.tri_bvh);
     UP(bvh_spheres, rec.bvh_spheres); UP(bvh_sphere_filter, rec.bvh_sphere_filter); UP(bvh_sphere_key, rec.bvh_sphere_key);
-    UP(bvh_tri_key, rec.bvh_tri_key); UP(bvh_tris, rec.bvh_tris);
+    UP(bvh_tri_key, rec.bvh_tri_key); UP(bvh_tris, rec.bvh_tris); UP(sphere_wide, hs.sphere_wide); UP(tri_wide, hs.tri_wide);
 #undef UP
     if (e != hipSuccess) return fail(RT_ERR_DEVICE, "scene upload: %s", hipGetErrorString(e));
     SceneView<R>& v = ds.view;
@@ -120,6 +122,7 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     v.plane_obj = ds.plane_obj.p; v.box_obj = ds.box_obj.p; v.sphere_nodes = ds.sphere_nodes.p; v.tri_nodes = ds.tri_nodes.p;
     v.bvh_spheres = ds.bvh_spheres.p; v.bvh_sphere_filter = ds.bvh_sphere_filter.p; v.bvh_sphere_key = ds.bvh_sphere_key.p;
     v.bvh_tris = ds.bvh_tris.p; v.bvh_tri_key = ds.bvh_tri_key.p;
+    v.sphere_wide = ds.sphere_wide.p; v.tri_wide = ds.tri_wide.p;
     fill_view_constants(v, hs, d);
     return RT_OK;
 }
@@ -196,11 +199,35 @@ ImageParams image_params(const rt_settings* s, int cw, int ch) {
 // primitives (Cornell) to 50k (mesh50k), DESIGN.md "BVH")
 constexpr int kAutoBvhPrims = 8;
 
+bool use_bvh(const rt_scene* sc, const rt_settings* s) {
+    return s->accel == RT_ACCEL_BVH || (s->accel == RT_ACCEL_AUTO && sc->bvh_prims >= kAutoBvhPrims);
+}
+
 hipError_t trace(rt_scene* sc, const rt_settings* s, const ImageParams& im, const Counters& c, hipStream_t st) {
     if (im.max_depth <= 0) return hipSuccess;   // rayColor(ray, depth<=0) is 0: nothing to trace
-    const bool bvh = s->accel == RT_ACCEL_BVH || (s->accel == RT_ACCEL_AUTO && sc->bvh_prims >= kAutoBvhPrims);
+    const bool bvh = use_bvh(sc, s);
     if (s->precision == RT_PREC_F32) return launch_trace<float>(sc->s32.view, im, c, bvh, st);
     return launch_trace<double>(sc->s64.view, im, c, bvh, st);
+}
+
+// totals = [segments, BVH nodes, sphere tests, triangle tests] of the launches
+void fill_stats(rt_stats* st, const rt_scene* sc, const rt_settings* s, const unsigned long long* totals, size_t n,
+                const ImageParams& im) {
+    st->samples = (uint64_t)n * (uint64_t)std::max(0, im.s_end - im.s_begin);
+    st->segments = totals[0];
+    if (use_bvh(sc, s)) {
+        const uint64_t brute = (uint64_t)sc->s64.view.num_planes + sc->s64.view.num_boxes;
+        st->node_visits = totals[1];
+        st->sphere_tests = totals[2];
+        st->tri_tests = totals[3];
+        st->prim_tests = totals[2] + totals[3] + totals[0] * brute;
+        st->algorithmic_bytes = 64.0 * totals[1] + 16.0 * totals[2] + 36.0 * totals[3] + 24.0 * totals[0] * brute +
+                                12.0 * (double)n;
+    } else {
+        st->node_visits = st->sphere_tests = st->tri_tests = 0;
+        st->prim_tests = totals[0] * (uint64_t)sc->num_prims;
+        st->algorithmic_bytes = (double)totals[0] * sc->record_bytes + 12.0 * (double)n;
+    }
 }
 
 }  // namespace
@@ -296,9 +323,9 @@ int rt_render(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progr
     const size_t n = (size_t)cw * ch;
     const bool want_segs = out && out->segments, want_draws = out && out->draws;
     HIP_TRY(sc->sum.ensure(3 * n));
-    HIP_TRY(sc->total.ensure(1));
+    HIP_TRY(sc->total.ensure(4));
     HIP_TRY(hipMemsetAsync(sc->sum.p, 0, 3 * n * sizeof(double), sc->stream));
-    HIP_TRY(hipMemsetAsync(sc->total.p, 0, sizeof(unsigned long long), sc->stream));
+    HIP_TRY(hipMemsetAsync(sc->total.p, 0, 4 * sizeof(unsigned long long), sc->stream));
     Counters c{sc->sum.p, nullptr, nullptr, sc->total.p};
     if (want_segs) {
         HIP_TRY(sc->segs.ensure(n));
@@ -343,18 +370,15 @@ int rt_render(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progr
     if (want_rgba) HIP_TRY(hipMemcpyAsync(out->rgba8, sc->rgba.p, 4 * n, hipMemcpyDeviceToHost, sc->stream));
     if (want_segs) HIP_TRY(hipMemcpyAsync(out->segments, sc->segs.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, sc->stream));
     if (want_draws) HIP_TRY(hipMemcpyAsync(out->draws, sc->draws.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, sc->stream));
-    unsigned long long total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, sc->total.p, sizeof total, hipMemcpyDeviceToHost, sc->stream));
+    unsigned long long totals[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(totals, sc->total.p, sizeof totals, hipMemcpyDeviceToHost, sc->stream));
     HIP_TRY(hipStreamSynchronize(sc->stream));
     if (stats) {
         float fms = 0;
         HIP_TRY(hipEventElapsedTime(&fms, sc->ev[2], sc->ev[3]));
         stats->kernel_ms = kernel_ms;
         stats->finalize_ms = fms;
-        stats->samples = (uint64_t)n * (uint64_t)std::max(0, s1 - s0);
-        stats->segments = total;
-        stats->prim_tests = total * (uint64_t)sc->num_prims;
-        stats->algorithmic_bytes = (double)total * sc->record_bytes + 12.0 * (double)n;
+        fill_stats(stats, sc, s, totals, n, im);
         stats->wall_ms = now_ms() - t_start;
     }
     return RT_OK;
@@ -368,27 +392,23 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
     if (rc) return rc;
     HIP_TRY(hipSetDevice(sc->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : sc->stream;
-    HIP_TRY(sc->total.ensure(1));
-    HIP_TRY(hipMemsetAsync(sc->total.p, 0, sizeof(unsigned long long), st));
+    HIP_TRY(sc->total.ensure(4));
+    HIP_TRY(hipMemsetAsync(sc->total.p, 0, 4 * sizeof(unsigned long long), st));
     ImageParams im = image_params(s, cw, ch);
     Counters c{d_sum, nullptr, nullptr, sc->total.p};
     HIP_TRY(hipEventRecord(sc->ev[0], st));
     HIP_TRY(trace(sc, s, im, c, st));
     HIP_TRY(hipEventRecord(sc->ev[1], st));
     if (sync || stats) {
-        unsigned long long total = 0;
-        HIP_TRY(hipMemcpyAsync(&total, sc->total.p, sizeof total, hipMemcpyDeviceToHost, st));
+        unsigned long long totals[4] = {0, 0, 0, 0};
+        HIP_TRY(hipMemcpyAsync(totals, sc->total.p, sizeof totals, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         if (stats) {
             float ms = 0;
             HIP_TRY(hipEventElapsedTime(&ms, sc->ev[0], sc->ev[1]));
-            const size_t n = (size_t)cw * ch;
             stats->kernel_ms = ms;
             stats->finalize_ms = 0;
-            stats->samples = (uint64_t)n * (uint64_t)std::max(0, im.s_end - im.s_begin);
-            stats->segments = total;
-            stats->prim_tests = total * (uint64_t)sc->num_prims;
-            stats->algorithmic_bytes = (double)total * sc->record_bytes + 12.0 * (double)n;
+            fill_stats(stats, sc, s, totals, (size_t)cw * ch, im);
             stats->wall_ms = now_ms() - t_start;
         }
     }

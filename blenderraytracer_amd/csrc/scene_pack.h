@@ -23,6 +23,7 @@ struct HostScene {   // precision-independent staging, binary64 as packed by the
     std::vector<double> tri_verts;                                // v0, v1, v2 as given (BVH bounds)
     std::vector<BvhNode> sphere_bvh, tri_bvh;                     // built by build_bvhs()
     std::vector<int> sphere_bvh_prims, tri_bvh_prims;
+    std::vector<Bvh2Node> sphere_wide, tri_wide;                  // the same trees, two-child nodes
     int num_prims = 0;
     double record_bytes = 0;      // SURVEY §8d canonical bytes tested per segment
 };
@@ -147,7 +148,16 @@ struct BvhBuilder {
         return x * y + y * z + z * x;
     }
 
-    int build(int begin, int end) {
+    // levels a median-split subtree of `count` primitives needs below its root
+    static int median_levels(int count) {
+        int l = 0;
+        for (long long c = (count + kLeafMax - 1) / kLeafMax; c > 1; c = (c + 1) / 2) ++l;
+        return l;
+    }
+
+    // depth: of this node (root 0).  Leaves stay at depth <= RT_BVH_STACK (the ordered walk's stack
+    // holds at most one entry per level): when SAH could go deeper, the split becomes a median.
+    int build(int begin, int end, int depth = 0) {
         const int me = (int)nodes.size();
         nodes.push_back(BvhNode{});
         double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -173,7 +183,8 @@ struct BvhBuilder {
             if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
         const double extent = chi[axis] - clo[axis];
         int mid = -1;
-        if (count > kLeafMax && extent > 0) {
+        const bool force_median = depth + 1 + median_levels(count) >= RT_BVH_STACK;
+        if (count > kLeafMax && extent > 0 && !force_median) {
             // binned SAH along the widest centroid axis
             struct Bin { double lo[3], hi[3]; int n; };
             Bin bins[kBins];
@@ -222,22 +233,60 @@ struct BvhBuilder {
                 std::nth_element(prims.begin() + begin, prims.begin() + mid, prims.begin() + end,
                                  [&](const BuildPrim& p, const BuildPrim& q) { return p.c[axis] < q.c[axis]; });
             }
-        } else if (count > kLeafMax) {              // all centroids equal: split by count
+        } else if (count > kLeafMax) {              // depth cap or all centroids equal: median split
             mid = (begin + end) / 2;
+            std::nth_element(prims.begin() + begin, prims.begin() + mid, prims.begin() + end,
+                             [&](const BuildPrim& p, const BuildPrim& q) { return p.c[axis] < q.c[axis]; });
         }
         if (mid < 0) {                              // leaf
             n.fc = ((int)order.size() << 4) | count;
             for (int k = begin; k < end; ++k) order.push_back(prims[k].idx);
         } else {
             n.fc = 0;
-            build(begin, mid);                      // first child = me + 1 (preorder)
-            build(mid, end);
+            build(begin, mid, depth + 1);           // first child = me + 1 (preorder)
+            build(mid, end, depth + 1);
         }
         n.skip = (int)nodes.size();                 // next node after this subtree
         nodes[me] = n;
         return me;
     }
 };
+
+// preorder BvhNode tree -> Bvh2Node array of its inner nodes (root first); a tree that is a single
+// leaf becomes one node whose second child is an empty leaf
+inline std::vector<Bvh2Node> make_wide(const std::vector<BvhNode>& t) {
+    std::vector<Bvh2Node> out;
+    if (t.empty()) return out;
+    auto box = [&](float* b, int i) {
+        for (int a = 0; a < 3; ++a) { b[a] = t[i].lo[a]; b[3 + a] = t[i].hi[a]; }
+    };
+    if (t[0].fc != 0) {
+        Bvh2Node n{};
+        box(n.box[0], 0);
+        box(n.box[1], 0);
+        n.child[0] = ~t[0].fc;
+        n.child[1] = ~0;                           // fc 0: no primitives
+        out.push_back(n);
+        return out;
+    }
+    std::vector<int> map(t.size(), -1);
+    int k = 0;
+    for (size_t i = 0; i < t.size(); ++i)
+        if (t[i].fc == 0) map[i] = k++;
+    out.resize(k);
+    auto ref = [&](int i) { return t[i].fc ? ~t[i].fc : map[i]; };
+    for (size_t i = 0; i < t.size(); ++i) {
+        if (t[i].fc != 0) continue;
+        const int l = (int)i + 1, r = t[l].skip;
+        Bvh2Node n{};
+        box(n.box[0], l);
+        box(n.box[1], r);
+        n.child[0] = ref(l);
+        n.child[1] = ref(r);
+        out[map[i]] = n;
+    }
+    return out;
+}
 
 inline void build_bvhs(HostScene& hs) {
     BvhBuilder sb;
@@ -269,6 +318,8 @@ inline void build_bvhs(HostScene& hs) {
     if (!tb.prims.empty()) tb.build(0, (int)tb.prims.size());
     hs.tri_bvh = std::move(tb.nodes);
     hs.tri_bvh_prims = std::move(tb.order);
+    hs.sphere_wide = make_wide(hs.sphere_bvh);
+    hs.tri_wide = make_wide(hs.tri_bvh);
 }
 
 // Record arrays of one precision (host memory); rt_capi.cpp uploads them, tests/hostcheck uses them.

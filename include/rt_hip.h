@@ -165,8 +165,14 @@ typedef struct rt_stats {
     double wall_ms;              /* host wall time of the call */
     uint64_t samples;            /* pixels x samples traced */
     uint64_t segments;           /* world.hit calls (ray segments) */
-    uint64_t prim_tests;         /* segments x primitives tested (brute force) */
-    double algorithmic_bytes;    /* segments x sum of primitive record bytes + 12 B/pixel framebuffer */
+    uint64_t prim_tests;         /* primitives tested: segments x primitives (brute force), counted (BVH) */
+    double algorithmic_bytes;    /* SURVEY §8(d) record bytes the tests read + 12 B/pixel framebuffer:
+                                    brute force: segments x sum of primitive record bytes;
+                                    BVH: 64 B/node visited + 16 B/sphere + 36 B/triangle tested
+                                    + segments x 24 B per plane and box */
+    uint64_t node_visits;        /* BVH nodes visited (0 for brute force) */
+    uint64_t sphere_tests;       /* BVH: sphere / triangle tests in visited leaves (0 for brute force) */
+    uint64_t tri_tests;
 } rt_stats;
 
 typedef struct rt_scene rt_scene;   /* opaque: scene resident in HBM of one device */

@@ -29,6 +29,7 @@ struct HostView {
         v.sphere_nodes = hs.sphere_bvh.data(); v.tri_nodes = hs.tri_bvh.data();
         v.bvh_spheres = rec.bvh_spheres.data(); v.bvh_sphere_filter = rec.bvh_sphere_filter.data();
         v.bvh_sphere_key = rec.bvh_sphere_key.data(); v.bvh_tris = rec.bvh_tris.data(); v.bvh_tri_key = rec.bvh_tri_key.data();
+        v.sphere_wide = hs.sphere_wide.data(); v.tri_wide = hs.tri_wide.data();
         fill_view_constants(v, hs, *d);
         return true;
     }
@@ -50,13 +51,19 @@ static int render(const rt_scene_desc* d, const rt_settings* s, double* sum, uin
     im.max_depth = s->max_depth;
     im.aa_mode = s->aa_mode;
     im.seedm = host_seed_mix(s->seed);
+    int stack[RT_BVH_STACK];
+    const BvhStack stk{stack, 1};
+    const LdsSpheres no_lds{nullptr};
     for (int cy = 0; cy < im.ch; ++cy)
         for (int cx = 0; cx < im.cw; ++cx) {
             const size_t q = (size_t)cy * im.cw + cx;
-            PixelResult r{0, 0};
+            PixelResult r{0, 0, {0, 0, 0}};
+            double* acc = sum + 3 * q;
+            // accel: RT_ACCEL_BVH = the ordered stack walk the library runs, 3 = the stackless walk
             if (im.max_depth > 0)
-                r = s->accel == RT_ACCEL_BVH ? trace_pixel<R, true, ACC_BVH>(v, im, cx, cy, im.s_end, sum + 3 * q)
-                                             : trace_pixel<R, true, ACC_BRUTE>(v, im, cx, cy, im.s_end, sum + 3 * q);
+                r = s->accel == RT_ACCEL_BVH ? trace_pixel<R, true, ACC_BVH_STACK>(v, im, cx, cy, im.s_end, acc, no_lds, stk)
+                  : s->accel == 3            ? trace_pixel<R, true, ACC_BVH>(v, im, cx, cy, im.s_end, acc)
+                                             : trace_pixel<R, true, ACC_BRUTE>(v, im, cx, cy, im.s_end, acc);
             segs[q] = r.segments;
             draws[q] = r.draws;
         }
@@ -173,11 +180,16 @@ extern "C" long long ptc_bvh_check(const rt_scene_desc* d, long long n, unsigned
         const double dl = std::pow(10.0, 2.0 * U(gen));
         V3<double> O{o[0], o[1], o[2]}, D{(target[0] - o[0]) * dl, (target[1] - o[1]) * dl, (target[2] - o[2]) * dl};
         const Closest<double> a = closest_hit<double, false>(v, O, D);
-        const Closest<double> b = closest_hit_bvh(v, O, D);
+        Work w{0, 0, 0};
+        int stack[RT_BVH_STACK];
+        const Closest<double> b = closest_hit_bvh<double, false>(v, O, D, w, BvhStack{nullptr, 0});
+        const Closest<double> c = closest_hit_bvh<double, true>(v, O, D, w, BvhStack{stack, 1});
         if (a.kind != HIT_NONE) ++nh;
-        const bool same = a.kind == b.kind && (a.kind == HIT_NONE || (a.idx == b.idx && a.mat == b.mat &&
-                                                                     std::memcmp(&a.t, &b.t, 8) == 0));
-        bad += !same;
+        for (const Closest<double>& x : {b, c}) {
+            const bool same = a.kind == x.kind && (a.kind == HIT_NONE || (a.idx == x.idx && a.mat == x.mat &&
+                                                                         std::memcmp(&a.t, &x.t, 8) == 0));
+            bad += !same;
+        }
     }
     if (hits) *hits = nh;
     return bad;
