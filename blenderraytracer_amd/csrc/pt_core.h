@@ -119,8 +119,9 @@ struct SceneView {
     int num_tri_nodes;
     const TriRec<R>* bvh_tris;
     const PrimKey* bvh_tri_key;
-    const Bvh2Node* sphere_wide;   // null when there are no spheres
-    const Bvh2Node* tri_wide;      // null when there are no triangles
+    const Bvh2Node* sphere_wide;   // breadth-first two-child nodes of the two trees
+    const Bvh2Node* tri_wide;
+    int num_sphere_wide, num_tri_wide;
     // camera (camera.js:8-36 vectors, computed on the host in binary64)
     R cam_o[3], cam_llc[3], cam_h[3], cam_v[3], cam_u[3], cam_vv[3], cam_w[3];
     R lens_radius;
@@ -337,7 +338,9 @@ RT_HD bool triangle_candidate(const TriRec<R>& tr, V3<R> o, V3<R> d, R tmin, R& 
 // the current best is never culled; f64 mode stays bit-identical to the brute-force walk
 // (tests/test_hostcheck.py, tests/test_gpu_parity.py).  Directions with a binary32-denormal
 // component are clamped to 1/d = 2^126 (t ranges beyond 2^100 are not modelled).
-struct BvhRay { float olo[3], ohi[3], inv[3]; };
+// The two-child walk evaluates (lo - olo) * inv as fma(lo, inv, -olo * inv): one rounding of olo*inv
+// more, an error < 2^-23 (|o| + |lo|) |inv| in t, still 16x inside the same margins.
+struct BvhRay { float olo[3], ohi[3], inv[3], slo[3], shi[3]; };   // slo = olo * inv, shi = ohi * inv
 
 template <class R>
 RT_HD BvhRay make_bvh_ray(V3<R> o, V3<R> d) {
@@ -352,6 +355,8 @@ RT_HD BvhRay make_bvh_ray(V3<R> o, V3<R> d) {
         float inv = 1.0f / df[k];
         if (!(fabsf(inv) <= 0x1p126f)) inv = copysignf(0x1p126f, df[k]);
         r.inv[k] = inv;
+        r.slo[k] = r.olo[k] * inv;
+        r.shi[k] = r.ohi[k] * inv;
     }
     return r;
 }
@@ -387,10 +392,19 @@ struct Work { uint32_t nodes, spheres, tris; };   // BVH nodes visited, sphere /
 // GPU, strided by the workgroup size so a wave's accesses are conflict-free)
 struct BvhStack { int* base; int stride; };
 
+#ifndef RT_BVH_FMA
+#define RT_BVH_FMA 1
+#endif
 RT_HD bool bvh_box_hit(const float* bx, const BvhRay& r, float tlimit, float& tn) {
+#if RT_BVH_FMA
+    const float x0 = __builtin_fmaf(bx[0], r.inv[0], -r.slo[0]), x1 = __builtin_fmaf(bx[3], r.inv[0], -r.shi[0]);
+    const float y0 = __builtin_fmaf(bx[1], r.inv[1], -r.slo[1]), y1 = __builtin_fmaf(bx[4], r.inv[1], -r.shi[1]);
+    const float z0 = __builtin_fmaf(bx[2], r.inv[2], -r.slo[2]), z1 = __builtin_fmaf(bx[5], r.inv[2], -r.shi[2]);
+#else
     const float x0 = (bx[0] - r.olo[0]) * r.inv[0], x1 = (bx[3] - r.ohi[0]) * r.inv[0];
     const float y0 = (bx[1] - r.olo[1]) * r.inv[1], y1 = (bx[4] - r.ohi[1]) * r.inv[1];
     const float z0 = (bx[2] - r.olo[2]) * r.inv[2], z1 = (bx[5] - r.ohi[2]) * r.inv[2];
+#endif
     tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.0f));
     const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tlimit));
     return tn <= tf;

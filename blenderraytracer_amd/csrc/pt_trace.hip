@@ -35,7 +35,8 @@ void trace_kernel(const TraceArgs<R> args) {
     if constexpr (ACC == ACC_BVH_STACK) {
         // per-lane traversal stacks, entry k of thread t at [k * 256 + t] (32 KB per workgroup)
         __shared__ int bvh_stack[RT_BVH_STACK * 256];
-        stk = BvhStack{bvh_stack + threadIdx.x, 256};
+        stk.base = bvh_stack + threadIdx.x;
+        stk.stride = 256;
     }
     if constexpr (ACC == ACC_LDS) {
         // stage the binary32 sphere filter records of the whole scene in LDS (one copy per workgroup)

@@ -140,8 +140,14 @@ struct BvhBuilder {
     std::vector<BuildPrim> prims;
     std::vector<BvhNode> nodes;
     std::vector<int> order;
-    static constexpr int kLeafMax = 4;
-    static constexpr int kBins = 16;
+#ifndef RT_BVH_LEAF
+#define RT_BVH_LEAF 2             // measured: 1 / 2 / 4 / 8 within 3 % on RTOW, 2 best on mesh50k
+#endif
+#ifndef RT_BVH_BINS
+#define RT_BVH_BINS 16
+#endif
+    static constexpr int kLeafMax = RT_BVH_LEAF;   // primitives per leaf (<= 15)
+    static constexpr int kBins = RT_BVH_BINS;      // SAH bins
 
     static double area(const double* lo, const double* hi) {
         const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
@@ -252,8 +258,9 @@ struct BvhBuilder {
     }
 };
 
-// preorder BvhNode tree -> Bvh2Node array of its inner nodes (root first); a tree that is a single
-// leaf becomes one node whose second child is an empty leaf
+// preorder BvhNode tree -> Bvh2Node array of its inner nodes in preorder (root first); a tree that
+// is a single leaf becomes one node whose second child is an empty leaf.  (Breadth-first order with
+// the top levels staged in LDS measured no faster: the node loads hit L1/L2, DESIGN.md "BVH".)
 inline std::vector<Bvh2Node> make_wide(const std::vector<BvhNode>& t) {
     std::vector<Bvh2Node> out;
     if (t.empty()) return out;
@@ -271,7 +278,7 @@ inline std::vector<Bvh2Node> make_wide(const std::vector<BvhNode>& t) {
     }
     std::vector<int> map(t.size(), -1);
     int k = 0;
-    for (size_t i = 0; i < t.size(); ++i)
+    for (size_t i = 0; i < t.size(); ++i)           // preorder: a subtree's nodes stay close in memory
         if (t[i].fc == 0) map[i] = k++;
     out.resize(k);
     auto ref = [&](int i) { return t[i].fc ? ~t[i].fc : map[i]; };
@@ -408,6 +415,8 @@ void fill_view_constants(SceneView<R>& v, const HostScene& hs, const rt_scene_de
     v.num_boxes = (int)hs.box_mat.size();
     v.num_sphere_nodes = (int)hs.sphere_bvh.size();
     v.num_tri_nodes = (int)hs.tri_bvh.size();
+    v.num_sphere_wide = (int)hs.sphere_wide.size();
+    v.num_tri_wide = (int)hs.tri_wide.size();
     const rt_camera_desc& c = d.camera;
     for (int k = 0; k < 3; ++k) {
         v.cam_o[k] = (R)c.origin[k];
