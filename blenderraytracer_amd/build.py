@@ -18,7 +18,7 @@ REPO = os.path.dirname(HERE)
 ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 
-SOURCES = ["pt_trace.hip", "rt_capi.cpp"]
+SOURCES = ["pt_trace.hip", "rt_capi.cpp", "scene_json.cpp"]
 HIP_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
              "-Wall", "-Wno-unused-function", "-I", os.path.join(REPO, "include")]
 
@@ -38,7 +38,7 @@ def _stale(target, deps):
 def build_lib(force=False):
     os.makedirs(LIBDIR, exist_ok=True)
     target = os.path.join(LIBDIR, "librt_hip.so")
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(REPO, "include", "rt_hip.h")]
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(REPO, "include", f) for f in os.listdir(os.path.join(REPO, "include"))]
     if not force and not _stale(target, deps):
         return target
     objs = []

@@ -37,6 +37,17 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
+}  // namespace
+
+namespace rt {
+int set_error(int code, const char* msg) {   // for the other translation units (scene_json.cpp)
+    g_error = msg;
+    return code;
+}
+}  // namespace rt
+
+namespace {
+
 #define HIP_TRY(expr)                                                                         \
     do {                                                                                      \
         hipError_t e_ = (expr);                                                               \

@@ -110,7 +110,7 @@ class Camera:
 def _material(m):  # scene-loader.js:143-173 + materials.js constructors
     if not m or not isinstance(m, dict) or not truthy(m.get("type")):
         return ("lambertian", (0.8, 0.8, 0.8))
-    t = str(m["type"]).lower()
+    t = _js_lower(m["type"], "material")
     if t == "lambertian":
         return ("lambertian", parse_vec3(m.get("color")))
     if t == "metal":
@@ -163,11 +163,20 @@ def _mesh(vertices, indices):  # geometry.js:193-237
     return tris
 
 
+def _js_lower(t, what):
+    """`x.type.toLowerCase()`: throws (so loadFromJSON returns false) unless x.type is a string."""
+    if not isinstance(t, str):
+        raise TypeError(f"{what}.type.toLowerCase is not a function")
+    return t.lower()
+
+
 def _create_object(o, world):  # scene-loader.js:90-137
+    if o is None:
+        raise TypeError("Cannot read property 'type' of null")
     if not isinstance(o, dict) or not truthy(o.get("type")):
         return
     mat = _material(o.get("material") if truthy(o.get("material")) else {"type": "lambertian", "color": [0.8, 0.8, 0.8]})
-    t = str(o["type"]).lower()
+    t = _js_lower(o["type"], "object")
     if t == "sphere":
         world.add("sphere", mat, (parse_vec3(o.get("center")), num(js_or(o.get("radius"), 1.0))))
     elif t == "plane":

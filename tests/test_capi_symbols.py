@@ -9,13 +9,17 @@ from blenderraytracer_amd import capi
 from blenderraytracer_amd.scene import PackedScene, default_scene
 from blenderraytracer_amd.rng import permutation
 
-HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "rt_hip.h")
+INCLUDE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+HEADER = os.path.join(INCLUDE, "rt_hip.h")
 
 
 def declared_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return set(re.findall(r"^\s*(?:int|void|const char\*)\s+(rt_\w+)\s*\(", src, flags=re.M))
+    """Every function declared by include/*.h."""
+    names = set()
+    for h in sorted(os.listdir(INCLUDE)):
+        src = re.sub(r"/\*.*?\*/", "", open(os.path.join(INCLUDE, h)).read(), flags=re.S)
+        names |= set(re.findall(r"^\s*(?:int|void|const char\*|const rt_\w+\*)\s+(rt_\w+)\s*\(", src, flags=re.M))
+    return names
 
 
 def test_header_and_binding_agree():
