@@ -67,10 +67,24 @@ def build_napi(force=False):
     return target
 
 
+def build_cli(force=False):
+    """rt_render_cli: the Node-free front end (scene JSON -> rt_json_scene_load -> rt_render)."""
+    target = os.path.join(LIBDIR, "rt_render_cli")
+    src = os.path.join(CSRC, "rt_cli.cpp")
+    deps = [src, os.path.join(LIBDIR, "librt_hip.so")] + [os.path.join(REPO, "include", f)
+                                                          for f in os.listdir(os.path.join(REPO, "include"))]
+    if not force and not _stale(target, deps):
+        return target
+    _run(["g++", "-O2", "-std=c++17", "-Wall", "-I", os.path.join(REPO, "include"), src, "-o", target,
+          "-L", LIBDIR, "-lrt_hip", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath-link,/opt/rocm/lib"])
+    return target
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     force = "--force" in argv
     print(build_lib(force))
+    print(build_cli(force))
     if "--napi" in argv:
         print(build_napi(force))
 
