@@ -86,6 +86,9 @@ EXPORTS = {
     "rt_finalize_device": (C.c_int, [C.c_void_p, C.POINTER(Settings), C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p]),
     "rt_cancel": (C.c_int, [C.c_void_p]),
+    "rt_render_checkpoint": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_size_t, C.POINTER(C.c_int32)]),
+    "rt_render_resume": (C.c_int, [C.c_void_p, C.POINTER(Settings), C.POINTER(C.c_double), C.c_int32,
+                                   C.POINTER(Output), PROGRESS_FN, C.c_void_p, C.POINTER(Stats)]),
     # include/rt_scene_json.h (host-only scene-JSON loader)
     "rt_json_scene_load": (C.c_int, [C.c_char_p, C.c_size_t, C.c_int32, C.c_int32, C.c_uint32, C.POINTER(C.c_void_p)]),
     "rt_json_scene_desc": (C.POINTER(SceneDesc), [C.c_void_p]),

@@ -89,6 +89,7 @@ bool get_bytes(napi_env env, napi_value obj, const char* key, void** data, size_
 struct SceneBox {
     rt_scene* sc = nullptr;
     bool busy = false;
+    size_t last_pixels = 0;         // crop pixels of the last render (checkpoint size)
 };
 
 void scene_finalize(napi_env, void* data, void*) {
@@ -176,6 +177,8 @@ struct RenderJob {
     int status = 0;
     std::string error;
     std::atomic<int> cancel_from_js{0};
+    std::vector<double> resume;     // settings.resumeSums (rt_render_resume)
+    int32_t resume_done = -1;
 };
 
 void call_progress(napi_env env, napi_value js_cb, void*, void* data) {
@@ -212,7 +215,11 @@ void execute(napi_env, void* data) {
         out.segments = job->segs.data();
         out.draws = job->draws.data();
     }
-    job->status = rt_render(job->scene, &job->st, &out, progress_hook, job, &job->stats);
+    if (job->resume_done >= 0)
+        job->status = rt_render_resume(job->scene, &job->st, job->resume.data(), job->resume_done, &out, progress_hook,
+                                       job, &job->stats);
+    else
+        job->status = rt_render(job->scene, &job->st, &out, progress_hook, job, &job->stats);
     if (job->status != RT_OK) job->error = rt_last_error();
 }
 
@@ -308,6 +315,17 @@ napi_value render(napi_env env, napi_callback_info info) {
         return throw_err(env, "render: width/height must be positive");
     }
     job->n = (size_t)cw * ch;
+    void* rs = nullptr;
+    size_t rs_bytes = 0;
+    if (get_bytes(env, s, "resumeSums", &rs, &rs_bytes)) {        // continue from checkpoint(scene)
+        if (rs_bytes != job->n * 3 * sizeof(double)) {
+            delete job;
+            return throw_err(env, "render: resumeSums must hold 3 float64 per pixel of the frame");
+        }
+        job->resume.assign(static_cast<double*>(rs), static_cast<double*>(rs) + job->n * 3);
+        job->resume_done = (int32_t)get_num(env, s, "resumeSamplesDone", 0);
+    }
+    box->last_pixels = job->n;
     napi_value promise, name;
     NAPI_OK(napi_create_promise(env, &job->deferred, &promise));
     NAPI_OK(napi_create_reference(env, argv[0], 1, &job->scene_ref));
@@ -333,6 +351,27 @@ napi_value cancel(napi_env env, napi_callback_info info) {
     if (!box) return throw_err(env, "cancel(scene)");
     if (box->sc) rt_cancel(box->sc);
     return nullptr;
+}
+
+// checkpoint(scene) -> {sums: Float64Array(3 per pixel), samplesDone}: the progressive state after a
+// finished or cancelled render (rt_render_checkpoint); render(scene, {..., resumeSums, resumeSamplesDone})
+// continues from it
+napi_value checkpoint(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    SceneBox* box = argc ? get_box(env, argv[0]) : nullptr;
+    if (!box || !box->sc) return throw_err(env, "checkpoint(scene)");
+    if (box->busy) return throw_err(env, "checkpoint: a render is in flight");
+    std::vector<double> sums(box->last_pixels * 3);
+    int32_t done = 0;
+    if (rt_render_checkpoint(box->sc, sums.data(), sums.size(), &done) != RT_OK) return throw_err(env, rt_last_error());
+    napi_value res, d;
+    NAPI_OK(napi_create_object(env, &res));
+    NAPI_OK(napi_set_named_property(env, res, "sums", to_typed(env, sums, napi_float64_array)));
+    NAPI_OK(napi_create_int32(env, done, &d));
+    NAPI_OK(napi_set_named_property(env, res, "samplesDone", d));
+    return res;
 }
 
 napi_value destroy_scene(napi_env env, napi_callback_info info) {
@@ -366,6 +405,7 @@ napi_value init(napi_env env, napi_value exports) {
         {"createScene", nullptr, create_scene, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"render", nullptr, render, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"cancel", nullptr, cancel, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"checkpoint", nullptr, checkpoint, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"destroyScene", nullptr, destroy_scene, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"deviceCount", nullptr, device_count, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"abiVersion", nullptr, abi_version, nullptr, nullptr, nullptr, napi_enumerable, nullptr},

@@ -160,6 +160,8 @@ struct rt_scene {
     DevBuf<uint32_t> segs, draws;
     DevBuf<unsigned long long> total;
     std::atomic<int> cancel{0};
+    size_t ckpt_pixels = 0;         // progressive state of the last rt_render / rt_render_resume:
+    int ckpt_done = 0;              // `sum` holds samples [sample_begin, ckpt_done) of ckpt_pixels pixels
 };
 
 namespace {
@@ -322,8 +324,13 @@ int rt_cancel(rt_scene* sc) {
     return RT_OK;
 }
 
-int rt_render(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progress_fn progress, void* user,
-              rt_stats* stats) {
+}  // extern "C"
+
+namespace {
+
+// rt_render and rt_render_resume: trace samples [first, sample_end) on top of `sums_in` (NULL: zeros)
+int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progress_fn progress, void* user,
+                rt_stats* stats, const double* sums_in, int first) {
     const double t_start = now_ms();
     if (!sc) return fail(RT_ERR_INVALID, "scene is NULL");
     int cw, ch;
@@ -335,7 +342,8 @@ int rt_render(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progr
     const bool want_segs = out && out->segments, want_draws = out && out->draws;
     HIP_TRY(sc->sum.ensure(3 * n));
     HIP_TRY(sc->total.ensure(4));
-    HIP_TRY(hipMemsetAsync(sc->sum.p, 0, 3 * n * sizeof(double), sc->stream));
+    if (sums_in) HIP_TRY(hipMemcpyAsync(sc->sum.p, sums_in, 3 * n * sizeof(double), hipMemcpyHostToDevice, sc->stream));
+    else HIP_TRY(hipMemsetAsync(sc->sum.p, 0, 3 * n * sizeof(double), sc->stream));
     HIP_TRY(hipMemsetAsync(sc->total.p, 0, 4 * sizeof(unsigned long long), sc->stream));
     Counters c{sc->sum.p, nullptr, nullptr, sc->total.p};
     if (want_segs) {
@@ -349,8 +357,11 @@ int rt_render(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progr
         c.draws = sc->draws.p;
     }
     ImageParams im = image_params(s, cw, ch);
-    const int s0 = im.s_begin, s1 = im.s_end;
+    im.s_begin = std::max(im.s_begin, first);
+    const int s0 = im.s_begin, s1 = std::max(im.s_end, s0);
     const int batch = s->batch_samples > 0 ? s->batch_samples : std::max(1, s1 - s0);
+    sc->ckpt_pixels = n;
+    sc->ckpt_done = s0;
     double kernel_ms = 0;
     for (int b = s0; b < s1; b += batch) {
         ImageParams bi = im;
@@ -363,6 +374,7 @@ int rt_render(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progr
         float ms = 0;
         HIP_TRY(hipEventElapsedTime(&ms, sc->ev[0], sc->ev[1]));
         kernel_ms += ms;
+        sc->ckpt_done = bi.s_end;
         if (progress && bi.s_end < s1) {
             if (progress((double)(bi.s_end - s0) / (double)(s1 - s0), user)) sc->cancel.store(1);
         }
@@ -393,6 +405,35 @@ int rt_render(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progr
         stats->wall_ms = now_ms() - t_start;
     }
     return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_render(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progress_fn progress, void* user,
+              rt_stats* stats) {
+    return render_impl(sc, s, out, progress, user, stats, nullptr, 0);
+}
+
+int rt_render_checkpoint(rt_scene* sc, double* sums, size_t count, int32_t* samples_done) {
+    if (!sc || !sums || !samples_done) return fail(RT_ERR_INVALID, "NULL argument");
+    if (sc->ckpt_pixels == 0) return fail(RT_ERR_INVALID, "no render to checkpoint");
+    if (count != 3 * sc->ckpt_pixels)
+        return fail(RT_ERR_INVALID, "checkpoint holds %zu doubles, caller gave %zu", 3 * sc->ckpt_pixels, count);
+    HIP_TRY(hipSetDevice(sc->device));
+    HIP_TRY(hipMemcpyAsync(sums, sc->sum.p, count * sizeof(double), hipMemcpyDeviceToHost, sc->stream));
+    HIP_TRY(hipStreamSynchronize(sc->stream));
+    *samples_done = sc->ckpt_done;
+    return RT_OK;
+}
+
+int rt_render_resume(rt_scene* sc, const rt_settings* s, const double* sums, int32_t samples_done,
+                     const rt_output* out, rt_progress_fn progress, void* user, rt_stats* stats) {
+    if (!sums) return fail(RT_ERR_INVALID, "sums is NULL");
+    if (s && (samples_done < std::max(0, s->sample_begin) || samples_done > s->samples))
+        return fail(RT_ERR_INVALID, "samples_done %d outside [sample_begin, samples]", samples_done);
+    return render_impl(sc, s, out, progress, user, stats, sums, samples_done);
 }
 
 int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip_stream, int sync, rt_stats* stats) {

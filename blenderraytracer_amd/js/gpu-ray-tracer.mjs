@@ -45,6 +45,8 @@ export function settingsOf(rt, opts = {}) {
         precision: PRECISION[opts.precision || 'f64'],
         batchSamples: opts.batchSamples || 0,
         accel: ACCEL[opts.accel || 'auto'],
+        // continue a cancelled render from its checkpoint ({sums, samplesDone}, rt_render_resume)
+        ...(opts.resume ? { resumeSums: opts.resume.sums, resumeSamplesDone: opts.resume.samplesDone } : {}),
         cropX0: opts.crop ? opts.crop[0] : 0, cropY0: opts.crop ? opts.crop[1] : 0,
         cropW: opts.crop ? opts.crop[2] : 0, cropH: opts.crop ? opts.crop[3] : 0,
         wantMean: opts.wantMean ? 1 : 0, wantCounts: opts.wantCounts ? 1 : 0,
@@ -69,7 +71,11 @@ export async function gpuRender(rt, onProgress, opts = {}) {
         });
         return res;
     } catch (e) {
-        if (e && e.status === -4) return null;                    // RT_ERR_CANCELLED
+        if (e && e.status === -4) {                               // RT_ERR_CANCELLED
+            // keep the progressive state: render({resume: rt.checkpointState}) continues from it
+            rt.checkpointState = nat.checkpoint(scene);
+            return null;
+        }
         throw e;
     } finally {
         nat.destroyScene(scene);
@@ -151,6 +157,17 @@ export class GpuRayTracer {
     async render(onProgress) {
         const res = await gpuRender(this, onProgress, this.opts);
         if (!res) return;
+        blit(this, res);
+        this.lastStats = res.stats;
+        if (onProgress) onProgress(1.0);
+    }
+
+    // Continue the last cancelled render (window.renderCancelled) from its checkpoint.
+    async resume(onProgress) {
+        if (!this.checkpointState) return this.render(onProgress);
+        const res = await gpuRender(this, onProgress, { ...this.opts, resume: this.checkpointState });
+        if (!res) return;
+        this.checkpointState = null;
         blit(this, res);
         this.lastStats = res.stats;
         if (onProgress) onProgress(1.0);

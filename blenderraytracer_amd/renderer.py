@@ -123,9 +123,10 @@ class GpuRayTracer:
             self._dirty = False
         return self._scene
 
-    def render(self, on_progress=None, crop=None, want=("rgba8",), batch_samples=0):
+    def render(self, on_progress=None, crop=None, want=("rgba8",), batch_samples=0, resume=None):
         """RayTracer.render: fills image_data (RGBA8) and float_data (post-gamma RGBA float).
-        Returns a dict of the requested host arrays (mean, post, rgba8, segments, draws)."""
+        Returns a dict of the requested host arrays (mean, post, rgba8, segments, draws).
+        resume: a checkpoint() result to continue from (rt_render_resume)."""
         lib = capi.load_library()
         scene = self.scene_handle()
         st = self.settings(crop=crop, batch_samples=batch_samples)
@@ -149,7 +150,14 @@ class GpuRayTracer:
             out.draws = res["draws"].ctypes.data_as(C.POINTER(C.c_uint32))
         stats = capi.Stats()
         cb = capi.PROGRESS_FN(lambda f, u: int(bool(on_progress(f)) if on_progress else 0))
-        capi.check(lib.rt_render(scene, C.byref(st), C.byref(out), cb, None, C.byref(stats)))
+        if resume is None:
+            capi.check(lib.rt_render(scene, C.byref(st), C.byref(out), cb, None, C.byref(stats)))
+        else:
+            sums, done = resume
+            sums = np.ascontiguousarray(sums, dtype=np.float64)
+            assert sums.size == 3 * n, "checkpoint of another frame size"
+            capi.check(lib.rt_render_resume(scene, C.byref(st), sums.ctypes.data_as(C.POINTER(C.c_double)), int(done),
+                                            C.byref(out), cb, None, C.byref(stats)))
         self.last_stats = stats
         if crop is None:
             self.image_data = res["rgba8"]
@@ -158,6 +166,18 @@ class GpuRayTracer:
             on_progress(1.0)
         assert n == res["rgba8"].shape[0] * res["rgba8"].shape[1]
         return res
+
+    def checkpoint(self, crop=None):
+        """(per-pixel float64 sums (h, w, 3), samples_done) of the last render, finished or
+        cancelled (rt_render_checkpoint); pass it to render(resume=...) to continue."""
+        lib = capi.load_library()
+        st = self.settings(crop=crop)
+        cw, ch = st.crop_w or self.width, st.crop_h or self.height
+        sums = np.zeros((ch, cw, 3), dtype=np.float64)
+        done = C.c_int32()
+        capi.check(lib.rt_render_checkpoint(self.scene_handle(), sums.ctypes.data_as(C.POINTER(C.c_double)), sums.size,
+                                            C.byref(done)))
+        return sums, done.value
 
     def close(self):
         if self._scene is not None:

@@ -194,6 +194,17 @@ typedef int (*rt_progress_fn)(double fraction, void* user);
 int rt_render(rt_scene* scene, const rt_settings* settings, const rt_output* out,
               rt_progress_fn progress, void* user, rt_stats* stats);
 
+/* Progressive rendering (the reference's row-by-row progress, ray-tracer.js:258-261,
+ * at sample granularity).  After rt_render / rt_render_resume returns — finished or cancelled
+ * between sample batches (RT_ERR_CANCELLED) — the scene holds the per-pixel float64 radiance sums
+ * of samples [sample_begin, samples_done).  rt_render_checkpoint copies them out (count must be
+ * 3 x crop pixels) so a host can persist them; rt_render_resume traces samples
+ * [samples_done, sample_end) on top of such sums and finishes like rt_render.  Every pixel still
+ * adds its samples in order, so a resumed render is bit-identical to an uninterrupted one. */
+int rt_render_checkpoint(rt_scene* scene, double* sums, size_t count, int32_t* samples_done);
+int rt_render_resume(rt_scene* scene, const rt_settings* settings, const double* sums, int32_t samples_done,
+                     const rt_output* out, rt_progress_fn progress, void* user, rt_stats* stats);
+
 /* Device-level building blocks for multi-GPU (one process per GPU): trace samples
  * [sample_begin, sample_end) and ADD per-pixel radiance sums into d_sum (device, n*3 doubles,
  * caller zeroes it); segment counting goes to stats.  Asynchronous on `hip_stream`

@@ -56,6 +56,22 @@ if (cmd === 'pack') {
     const seen = [];
     await rt.render((f) => seen.push(f));
     summary._render = { progress: seen, nonzero: rt.imageData.data.some((v, i) => i % 4 !== 3 && v > 0) };
+    // progressive: window.renderCancelled mid-frame, then resume() from the checkpoint
+    {
+        const { rt: full } = tracerFor('kitchen_sink');
+        full.updateRenderSettings({ samples: 8 });
+        await full.render();
+        const { rt: part } = tracerFor('kitchen_sink', { batchSamples: 2 });
+        part.updateRenderSettings({ samples: 8 });
+        global.window = { renderCancelled: false };
+        let calls = 0;
+        await part.render(() => { if (++calls === 2) global.window.renderCancelled = true; });
+        const done = part.checkpointState ? part.checkpointState.samplesDone : -1;
+        global.window.renderCancelled = false;
+        await part.resume();
+        const a = full.imageData.data, b = part.imageData.data;
+        summary._resume = { samplesDone: done, equal: a.length === b.length && a.every((v, i) => v === b[i]) };
+    }
     fs.writeFileSync(path.join(outdir, 'summary.json'), JSON.stringify(summary));
 } else if (cmd === 'refpack') {
     // The drop-in: the reference's own RayTracer (temp copy prepared by the caller), its render()

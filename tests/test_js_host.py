@@ -152,3 +152,5 @@ def test_js_gpu_render_matches_reference(gpu):
             assert np.mean(ld("rgba8", np.uint8).reshape(ch, cw, 4) == gc.load_array(name, "rgba8")) >= 0.9999
         r = summary["_render"]
         assert r["progress"][-1] == 1.0 and r["nonzero"]
+        # window.renderCancelled after 2 of 4 batches, then GpuRayTracer.resume(): same image
+        assert summary["_resume"] == {"samplesDone": 4, "equal": True}
