@@ -152,5 +152,7 @@ def test_js_gpu_render_matches_reference(gpu):
             assert np.mean(ld("rgba8", np.uint8).reshape(ch, cw, 4) == gc.load_array(name, "rgba8")) >= 0.9999
         r = summary["_render"]
         assert r["progress"][-1] == 1.0 and r["nonzero"]
-        # window.renderCancelled after 2 of 4 batches, then GpuRayTracer.resume(): same image
-        assert summary["_resume"] == {"samplesDone": 4, "equal": True}
+        # window.renderCancelled set in the 2nd of 4 progress callbacks (delivered asynchronously, so
+        # the worker may finish one more batch), then GpuRayTracer.resume(): the same image
+        assert summary["_resume"]["equal"] is True
+        assert summary["_resume"]["samplesDone"] in (4, 6)
