@@ -82,9 +82,11 @@ struct BvhNode { float lo[3]; int skip; float hi[3]; int fc; };
 struct PrimKey { int id, obj; };   // index into the World-order arrays, World.objects index
 // The same tree as 64-B two-child nodes for the ordered stack walk: box k = {lo, hi} of child k,
 // child[k] >= 0 an inner node, < 0 the leaf ~fc.  Depth <= RT_BVH_STACK (scene_pack.h).
-struct Bvh2Node { float box[2][6]; int child[2]; int pad[2]; };
+// Bounds interleaved by child (lo[axis][child]) so both children's planes of an axis form one float2:
+// the slab test is 6 packed FMAs (v_pk_fma_f32) per node.
+struct Bvh2Node { float lo[3][2]; float hi[3][2]; int child[2]; int pad[2]; };
 #ifndef RT_BVH_STACK
-#define RT_BVH_STACK 32
+#define RT_BVH_STACK 24           // 24 KB of LDS per 256-lane workgroup; trees up to ~16.7M primitives
 #endif
 
 template <class R>
@@ -410,6 +412,30 @@ RT_HD bool bvh_box_hit(const float* bx, const BvhRay& r, float tlimit, float& tn
     return tn <= tf;
 }
 
+typedef float rt_f2 __attribute__((ext_vector_type(2)));
+#ifndef RT_BVH_WHILE_WHILE
+#define RT_BVH_WHILE_WHILE 0
+#endif
+
+// Both children of a two-child node: (lo - olo) * inv as fma(lo, inv, -olo * inv) for the pair of
+// children at once (same rounding as bvh_box_hit's FMA form).
+RT_HD void bvh_node2_hit(const Bvh2Node& n, const BvhRay& r, float tlimit, bool& h0, bool& h1, float& t0,
+                         float& t1) {
+    rt_f2 a[3], b[3];
+    for (int k = 0; k < 3; ++k) {
+        const rt_f2 inv = {r.inv[k], r.inv[k]};
+        const rt_f2 slo = {-r.slo[k], -r.slo[k]}, shi = {-r.shi[k], -r.shi[k]};
+        a[k] = __builtin_elementwise_fma(rt_f2{n.lo[k][0], n.lo[k][1]}, inv, slo);
+        b[k] = __builtin_elementwise_fma(rt_f2{n.hi[k][0], n.hi[k][1]}, inv, shi);
+    }
+    t0 = fmaxf(fmaxf(fminf(a[0].x, b[0].x), fminf(a[1].x, b[1].x)), fmaxf(fminf(a[2].x, b[2].x), 0.0f));
+    t1 = fmaxf(fmaxf(fminf(a[0].y, b[0].y), fminf(a[1].y, b[1].y)), fmaxf(fminf(a[2].y, b[2].y), 0.0f));
+    const float f0 = fminf(fminf(fmaxf(a[0].x, b[0].x), fmaxf(a[1].x, b[1].x)), fminf(fmaxf(a[2].x, b[2].x), tlimit));
+    const float f1 = fminf(fminf(fmaxf(a[0].y, b[0].y), fmaxf(a[1].y, b[1].y)), fminf(fmaxf(a[2].y, b[2].y), tlimit));
+    h0 = t0 <= f0;
+    h1 = t1 <= f1;
+}
+
 // Walk one BVH and call leaf(fc) for every leaf whose box the ray reaches before the current best.
 // WIDE: ordered walk over Bvh2Node (both child boxes per 64-B node, nearer child first, the other
 // pushed on the lane's stack); otherwise the stackless preorder walk over BvhNode skip links.
@@ -417,13 +443,46 @@ template <bool WIDE, class Leaf>
 RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const BvhRay& br, const float& tl,
                     BvhStack stk, Work& w, Leaf&& leaf) {
     if constexpr (WIDE) {
+#if RT_BVH_WHILE_WHILE
+        // "while-while": descend inner nodes until this lane holds a leaf (or its walk is over), then
+        // test the leaf; the wave runs the (binary64) leaf code once for all lanes holding one
+        // instead of in every inner-node iteration
+        int sp = 0, cur = 0;
+        bool live = true;
+        while (live) {
+            while (cur >= 0) {
+                const Bvh2Node n = wide[cur];
+                RT_COUNT(++w.nodes);
+                float t0, t1;
+                bool h0, h1;
+                bvh_node2_hit(n, br, tl, h0, h1, t0, t1);
+                if (h0 && h1) {
+                    const bool swap = t1 < t0;
+                    stk.base[(sp++) * stk.stride] = swap ? n.child[0] : n.child[1];
+                    cur = swap ? n.child[1] : n.child[0];
+                } else if (h0 | h1) {
+                    cur = h0 ? n.child[0] : n.child[1];
+                } else if (sp > 0) {
+                    cur = stk.base[(--sp) * stk.stride];
+                } else {
+                    live = false;
+                    break;
+                }
+            }
+            if (!live) break;
+            leaf(~cur);
+            if (sp == 0) break;
+            cur = stk.base[(--sp) * stk.stride];
+        }
+#else
         int sp = 0, cur = 0;
         for (;;) {
             if (cur >= 0) {
                 const Bvh2Node n = wide[cur];
                 RT_COUNT(++w.nodes);
                 float t0, t1;
-                const bool h0 = bvh_box_hit(n.box[0], br, tl, t0), h1 = bvh_box_hit(n.box[1], br, tl, t1);
+                bool h0, h1;
+                bvh_node2_hit(n, br, tl, h0, h1, t0, t1);
                 if (h0 && h1) {
                     const bool swap = t1 < t0;
                     stk.base[(sp++) * stk.stride] = swap ? n.child[0] : n.child[1];
@@ -440,6 +499,7 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
             if (sp == 0) break;
             cur = stk.base[(--sp) * stk.stride];
         }
+#endif
     } else {
         int ni = 0;
         while (ni < count) {

@@ -94,7 +94,18 @@ RT_HD bool scatter(const MatRec<R>& m, const Hit<R>& h, V3<R> d, Rng<R>& g, V3<R
     return true;
 }
 
-struct PixelResult { uint32_t segments, draws; Work work; };
+// RT_PROFILE=1 (A/B builds only): shader-clock cycles per lane spent in closest hit, shading and
+// sample regeneration, reduced per wave (max) into Counters::totals[4..6]
+#ifndef RT_PROFILE
+#define RT_PROFILE 0
+#endif
+#if RT_PROFILE && defined(__HIP_DEVICE_COMPILE__)
+#define RT_TICK() ((uint64_t)clock64())
+#else
+#define RT_TICK() ((uint64_t)0)
+#endif
+
+struct PixelResult { uint32_t segments, draws; Work work; uint64_t cyc[3]; };
 
 // Trace samples [im.s_begin, s_end) of crop pixel (cx, cy), adding radiance into sum[0..2].
 template <class R, bool COUNT, int ACC = ACC_BRUTE>
@@ -102,7 +113,7 @@ RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int
                               const LdsSpheres lds = LdsSpheres{nullptr}, BvhStack stk = BvhStack{nullptr, 0}) {
     const int i = im.x0 + cx, row = im.y0 + cy, j = im.height - 1 - row;
     const uint32_t pkey = pixel_key(im.seedm, (uint32_t)row * (uint32_t)im.width + (uint32_t)i);
-    PixelResult res{0, 0, {0, 0, 0}};
+    PixelResult res{0, 0, {0, 0, 0}, {0, 0, 0}};
     int s = im.s_begin;
     double sx = sum[0], sy = sum[1], sz = sum[2];
     Rng<R> g;
@@ -110,7 +121,10 @@ RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int
     int depth = im.max_depth;
     if (s < s_end) start_sample(sc, im, i, j, pkey, s, g, o, d);
     while (s < s_end) {
+        const uint64_t t0 = RT_TICK();
         const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, lds, res.work, stk);
+        const uint64_t t1 = RT_TICK();
+        if (RT_PROFILE) res.cyc[0] += t1 - t0;
         ++res.segments;
         bool done = true;
         V3<R> L = mk<R>(0, 0, 0);
@@ -132,6 +146,8 @@ RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int
             V3<R> bg = background(sc, d);                                     // world.background(ray)
             L = mk(T.x * bg.x, T.y * bg.y, T.z * bg.z);
         }
+        const uint64_t t2 = RT_TICK();
+        if (RT_PROFILE) res.cyc[1] += t2 - t1;
         if (done) {
             sx += (double)L.x; sy += (double)L.y; sz += (double)L.z;
             if (COUNT) res.draws += g.k;
@@ -140,6 +156,7 @@ RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int
             depth = im.max_depth;
             if (s < s_end) start_sample(sc, im, i, j, pkey, s, g, o, d);
         }
+        if (RT_PROFILE) res.cyc[2] += RT_TICK() - t2;
     }
     sum[0] = sx; sum[1] = sy; sum[2] = sz;
     return res;

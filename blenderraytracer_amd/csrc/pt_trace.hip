@@ -23,11 +23,19 @@ struct TraceArgs {
 #endif
 
 #ifndef RT_BVH_WAVES_PER_SIMD
-#define RT_BVH_WAVES_PER_SIMD 4   // the BVH walk keeps more live state: 128 VGPRs ("BVH")
+#define RT_BVH_WAVES_PER_SIMD 4   // binary64 BVH walk: 128 VGPRs (measured 3/4/5 waves: 3861/4065/3287)
+#endif
+#ifndef RT_BVH_WAVES_F32
+#define RT_BVH_WAVES_F32 5        // binary32 BVH walk: 96 VGPRs (measured 3/4/5 waves: 5362/5230/5506)
 #endif
 
+template <class R, int ACC>
+constexpr int waves_per_simd() {
+    return ACC >= ACC_BVH ? (sizeof(R) == 8 ? RT_BVH_WAVES_PER_SIMD : RT_BVH_WAVES_F32) : RT_MIN_WAVES_PER_SIMD;
+}
+
 template <class R, bool COUNT, int ACC>
-__global__ __launch_bounds__(256, ACC >= ACC_BVH ? RT_BVH_WAVES_PER_SIMD : RT_MIN_WAVES_PER_SIMD)
+__global__ __launch_bounds__(256, (waves_per_simd<R, ACC>()))
 void trace_kernel(const TraceArgs<R> args) {
     const ImageParams& im = args.im;
     LdsSpheres lds{nullptr};
@@ -69,6 +77,13 @@ void trace_kernel(const TraceArgs<R> args) {
             unsigned long long v = parts[k];
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
             if (lane == 0) atomicAdd(args.c.totals + k, v);
+        }
+        if constexpr (RT_PROFILE != 0) {
+            for (int k = 0; k < 3; ++k) {
+                unsigned long long v = r.cyc[k];
+                for (int off = 32; off > 0; off >>= 1) v = max(v, (unsigned long long)__shfl_xor(v, off));
+                if (lane == 0) atomicAdd(args.c.totals + 4 + k, v);
+            }
         }
     }
 }

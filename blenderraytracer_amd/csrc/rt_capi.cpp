@@ -151,6 +151,7 @@ struct rt_scene {
     DeviceScene<float> s32;
     int num_prims = 0;
     int bvh_prims = 0;              // spheres + triangles (the primitives the BVHs cover)
+    bool bvh_ok = true;             // both trees fit the traversal stack (depth <= RT_BVH_STACK)
     double record_bytes = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {};
@@ -213,7 +214,15 @@ ImageParams image_params(const rt_settings* s, int cw, int ch) {
 constexpr int kAutoBvhPrims = 8;
 
 bool use_bvh(const rt_scene* sc, const rt_settings* s) {
+    if (!sc->bvh_ok) return false;
     return s->accel == RT_ACCEL_BVH || (s->accel == RT_ACCEL_AUTO && sc->bvh_prims >= kAutoBvhPrims);
+}
+
+int check_accel(const rt_scene* sc, const rt_settings* s) {
+    if (s->accel == RT_ACCEL_BVH && !sc->bvh_ok)
+        return fail(RT_ERR_INVALID, "BVH deeper than the %d-entry traversal stack (too many primitives): use "
+                    "RT_ACCEL_AUTO or RT_ACCEL_BRUTE", RT_BVH_STACK);
+    return RT_OK;
 }
 
 hipError_t trace(rt_scene* sc, const rt_settings* s, const ImageParams& im, const Counters& c, hipStream_t st) {
@@ -289,6 +298,7 @@ int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out) {
     sc->device = device;
     sc->num_prims = hs.num_prims;
     sc->bvh_prims = (int)(hs.sphere_r.size() + hs.tri_mat.size());
+    sc->bvh_ok = hs.bvh_depth <= RT_BVH_STACK;
     sc->record_bytes = hs.record_bytes;
     if ((rc = build_device(sc->s64, hs, *desc)) || (rc = build_device(sc->s32, hs, *desc))) {
         rt_scene_destroy(sc);
@@ -335,16 +345,17 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     if (!sc) return fail(RT_ERR_INVALID, "scene is NULL");
     int cw, ch;
     int rc = check_settings(s, &cw, &ch);
+    if (!rc) rc = check_accel(sc, s);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(sc->device));
     sc->cancel.store(0);
     const size_t n = (size_t)cw * ch;
     const bool want_segs = out && out->segments, want_draws = out && out->draws;
     HIP_TRY(sc->sum.ensure(3 * n));
-    HIP_TRY(sc->total.ensure(4));
+    HIP_TRY(sc->total.ensure(8));
     if (sums_in) HIP_TRY(hipMemcpyAsync(sc->sum.p, sums_in, 3 * n * sizeof(double), hipMemcpyHostToDevice, sc->stream));
     else HIP_TRY(hipMemsetAsync(sc->sum.p, 0, 3 * n * sizeof(double), sc->stream));
-    HIP_TRY(hipMemsetAsync(sc->total.p, 0, 4 * sizeof(unsigned long long), sc->stream));
+    HIP_TRY(hipMemsetAsync(sc->total.p, 0, 8 * sizeof(unsigned long long), sc->stream));
     Counters c{sc->sum.p, nullptr, nullptr, sc->total.p};
     if (want_segs) {
         HIP_TRY(sc->segs.ensure(n));
@@ -393,7 +404,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     if (want_rgba) HIP_TRY(hipMemcpyAsync(out->rgba8, sc->rgba.p, 4 * n, hipMemcpyDeviceToHost, sc->stream));
     if (want_segs) HIP_TRY(hipMemcpyAsync(out->segments, sc->segs.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, sc->stream));
     if (want_draws) HIP_TRY(hipMemcpyAsync(out->draws, sc->draws.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, sc->stream));
-    unsigned long long totals[4] = {0, 0, 0, 0};
+    unsigned long long totals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(totals, sc->total.p, sizeof totals, hipMemcpyDeviceToHost, sc->stream));
     HIP_TRY(hipStreamSynchronize(sc->stream));
     if (stats) {
@@ -404,6 +415,11 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         fill_stats(stats, sc, s, totals, n, im);
         stats->wall_ms = now_ms() - t_start;
     }
+#if RT_PROFILE
+    const double cyc = (double)(totals[4] + totals[5] + totals[6]);
+    fprintf(stderr, "[rt_profile] wave-max cycles: closest hit %.3f, shading %.3f, regeneration %.3f (%.3e total)\n",
+            totals[4] / cyc, totals[5] / cyc, totals[6] / cyc, cyc);
+#endif
     return RT_OK;
 }
 
@@ -441,18 +457,19 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
     if (!sc || !d_sum) return fail(RT_ERR_INVALID, "NULL argument");
     int cw, ch;
     int rc = check_settings(s, &cw, &ch);
+    if (!rc) rc = check_accel(sc, s);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(sc->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : sc->stream;
-    HIP_TRY(sc->total.ensure(4));
-    HIP_TRY(hipMemsetAsync(sc->total.p, 0, 4 * sizeof(unsigned long long), st));
+    HIP_TRY(sc->total.ensure(8));
+    HIP_TRY(hipMemsetAsync(sc->total.p, 0, 8 * sizeof(unsigned long long), st));
     ImageParams im = image_params(s, cw, ch);
     Counters c{d_sum, nullptr, nullptr, sc->total.p};
     HIP_TRY(hipEventRecord(sc->ev[0], st));
     HIP_TRY(trace(sc, s, im, c, st));
     HIP_TRY(hipEventRecord(sc->ev[1], st));
     if (sync || stats) {
-        unsigned long long totals[4] = {0, 0, 0, 0};
+        unsigned long long totals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         HIP_TRY(hipMemcpyAsync(totals, sc->total.p, sizeof totals, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         if (stats) {

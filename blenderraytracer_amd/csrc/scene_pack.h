@@ -24,6 +24,7 @@ struct HostScene {   // precision-independent staging, binary64 as packed by the
     std::vector<BvhNode> sphere_bvh, tri_bvh;                     // built by build_bvhs()
     std::vector<int> sphere_bvh_prims, tri_bvh_prims;
     std::vector<Bvh2Node> sphere_wide, tri_wide;                  // the same trees, two-child nodes
+    int bvh_depth = 0;                                            // deepest leaf of either tree
     int num_prims = 0;
     double record_bytes = 0;      // SURVEY §8d canonical bytes tested per segment
 };
@@ -140,6 +141,7 @@ struct BvhBuilder {
     std::vector<BuildPrim> prims;
     std::vector<BvhNode> nodes;
     std::vector<int> order;
+    int max_depth = 0;                              // deepest leaf (root = 0)
 #ifndef RT_BVH_LEAF
 #define RT_BVH_LEAF 2             // measured: 1 / 2 / 4 / 8 within 3 % on RTOW, 2 best on mesh50k
 #endif
@@ -245,6 +247,7 @@ struct BvhBuilder {
                              [&](const BuildPrim& p, const BuildPrim& q) { return p.c[axis] < q.c[axis]; });
         }
         if (mid < 0) {                              // leaf
+            max_depth = std::max(max_depth, depth);
             n.fc = ((int)order.size() << 4) | count;
             for (int k = begin; k < end; ++k) order.push_back(prims[k].idx);
         } else {
@@ -264,13 +267,13 @@ struct BvhBuilder {
 inline std::vector<Bvh2Node> make_wide(const std::vector<BvhNode>& t) {
     std::vector<Bvh2Node> out;
     if (t.empty()) return out;
-    auto box = [&](float* b, int i) {
-        for (int a = 0; a < 3; ++a) { b[a] = t[i].lo[a]; b[3 + a] = t[i].hi[a]; }
+    auto box = [&](Bvh2Node& n, int k, int i) {    // child k's bounds = tree node i's
+        for (int a = 0; a < 3; ++a) { n.lo[a][k] = t[i].lo[a]; n.hi[a][k] = t[i].hi[a]; }
     };
     if (t[0].fc != 0) {
         Bvh2Node n{};
-        box(n.box[0], 0);
-        box(n.box[1], 0);
+        box(n, 0, 0);
+        box(n, 1, 0);
         n.child[0] = ~t[0].fc;
         n.child[1] = ~0;                           // fc 0: no primitives
         out.push_back(n);
@@ -286,8 +289,8 @@ inline std::vector<Bvh2Node> make_wide(const std::vector<BvhNode>& t) {
         if (t[i].fc != 0) continue;
         const int l = (int)i + 1, r = t[l].skip;
         Bvh2Node n{};
-        box(n.box[0], l);
-        box(n.box[1], r);
+        box(n, 0, l);
+        box(n, 1, r);
         n.child[0] = ref(l);
         n.child[1] = ref(r);
         out[map[i]] = n;
@@ -307,6 +310,7 @@ inline void build_bvhs(HostScene& hs) {
         sb.prims.push_back(p);
     }
     if (!sb.prims.empty()) sb.build(0, (int)sb.prims.size());
+    hs.bvh_depth = sb.max_depth;
     hs.sphere_bvh = std::move(sb.nodes);
     hs.sphere_bvh_prims = std::move(sb.order);
     BvhBuilder tb;
@@ -323,6 +327,7 @@ inline void build_bvhs(HostScene& hs) {
         tb.prims.push_back(p);
     }
     if (!tb.prims.empty()) tb.build(0, (int)tb.prims.size());
+    hs.bvh_depth = std::max(hs.bvh_depth, tb.max_depth);
     hs.tri_bvh = std::move(tb.nodes);
     hs.tri_bvh_prims = std::move(tb.order);
     hs.sphere_wide = make_wide(hs.sphere_bvh);

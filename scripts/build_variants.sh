@@ -4,15 +4,19 @@
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/blenderraytracer_amd/lib/variants
+SRCS="pt_trace.hip rt_capi.cpp scene_json.cpp"     # the same sources as blenderraytracer_amd/build.py
 mkdir -p "$OUT"
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC $flags -I "$ROOT/include" \
-    -c "$ROOT/blenderraytracer_amd/csrc/pt_trace.hip" -o "$OUT/$name.trace.o" &
-  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC $flags -I "$ROOT/include" \
-    -c "$ROOT/blenderraytracer_amd/csrc/rt_capi.cpp" -o "$OUT/$name.capi.o" &
+  objs=""
+  for src in $SRCS; do
+    obj="$OUT/$name.${src%.*}.o"
+    /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC $flags -I "$ROOT/include" \
+      -c "$ROOT/blenderraytracer_amd/csrc/$src" -o "$obj" &
+    objs="$objs $obj"
+  done
   wait
-  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$OUT/$name.so" "$OUT/$name.trace.o" "$OUT/$name.capi.o"
-  rm -f "$OUT/$name.trace.o" "$OUT/$name.capi.o"
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$OUT/$name.so" $objs
+  rm -f $objs
   echo "built $OUT/$name.so ($flags)"
 done
