@@ -121,7 +121,7 @@ struct SceneView {
     int num_tri_nodes;
     const TriRec<R>* bvh_tris;
     const PrimKey* bvh_tri_key;
-    const Bvh2Node* sphere_wide;   // breadth-first two-child nodes of the two trees
+    const Bvh2Node* sphere_wide;   // two-child nodes of the two trees (preorder)
     const Bvh2Node* tri_wide;
     int num_sphere_wide, num_tri_wide;
     // camera (camera.js:8-36 vectors, computed on the host in binary64)
@@ -377,10 +377,10 @@ RT_HD bool bvh_node_hit(const BvhNode& n, const BvhRay& r, float tlimit) {
     return tn <= tf;
 }
 
-// Closest hit through the BVHs: planes and boxes (usually few, often large) brute force first, then
-// the sphere BVH and the triangle BVH, each a stackless walk of the preorder node array.  Lanes walk
-// their own paths (per-lane node loads); leaf records are contiguous in leaf order.
-struct Work { uint32_t nodes, spheres, tris; };   // BVH nodes visited, sphere / triangle tests (stats)
+struct Work {
+    uint32_t nodes, spheres, tris;                // BVH nodes visited, sphere / triangle tests (stats)
+    uint32_t lane_trips, wave_trips;              // RT_PROFILE: walk iterations per lane / per wave
+};
 #ifndef RT_BVH_COUNT
 #define RT_BVH_COUNT 1
 #endif
@@ -477,6 +477,10 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
 #else
         int sp = 0, cur = 0;
         for (;;) {
+#if RT_PROFILE && defined(__HIP_DEVICE_COMPILE__)
+            ++w.lane_trips;                       // the first active lane counts the wave's iteration
+            if ((int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) ++w.wave_trips;
+#endif
             if (cur >= 0) {
                 const Bvh2Node n = wide[cur];
                 RT_COUNT(++w.nodes);
@@ -516,10 +520,9 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
 // Closest hit through the BVHs: planes and boxes (usually few, often large) brute force first, then
 // the sphere BVH and the triangle BVH.  Lanes walk their own paths (per-lane node loads); leaf
 // records are contiguous in leaf order.
-template <class R, bool WIDE>
-RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
-    const R tmin = (R)0.001;
-    Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
+// Planes and boxes (usually few, often large) brute force, with their World.objects index.
+template <class R>
+RT_HD void brute_planes_boxes(const SceneView<R>& sc, V3<R> o, V3<R> d, R tmin, Closest<R>& b) {
     for (int i = 0; i < sc.num_planes; ++i) {                                 // geometry.js:56-74
         const PlaneRec<R> p = sc.planes[i];
         R denom = p.nx * d.x + p.ny * d.y + p.nz * d.z;
@@ -548,42 +551,62 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
         const int obj = sc.box_obj[i];
         if (better(t, obj, i, b)) b = Closest<R>{t, HIT_BOX, i, sc.box_mat[i], obj};
     }
+}
+
+// The primitives of one BVH leaf (fc = (first << 4) | count) against the current best.
+template <class R>
+RT_HD void sphere_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R a, const FilterRay& fr, R tmin,
+                       Closest<R>& b, float& tl, Work& w) {
+    const int first = fc >> 4, end = first + (fc & 15);
+    RT_COUNT(w.spheres += end - first);
+    for (int k = first; k < end; ++k) {
+        if constexpr (sizeof(R) == 8)
+            if (!sphere_filter_pass(sc.bvh_sphere_filter[k], fr)) continue;
+        R t;
+        if (!sphere_candidate(sc.bvh_spheres[k], o, d, a, tmin, t)) continue;
+        const PrimKey key = sc.bvh_sphere_key[k];
+        if (better(t, key.obj, key.id, b)) {
+            b = Closest<R>{t, HIT_SPHERE, key.id, sc.sphere_mat[key.id], key.obj};
+            tl = bvh_tlimit(b.t);
+        }
+    }
+}
+
+template <class R>
+RT_HD void tri_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R tmin, Closest<R>& b, float& tl, Work& w) {
+    const int first = fc >> 4, end = first + (fc & 15);
+    RT_COUNT(w.tris += end - first);
+    for (int k = first; k < end; ++k) {
+        R t;
+        if (!triangle_candidate(sc.bvh_tris[k], o, d, tmin, t)) continue;
+        const PrimKey key = sc.bvh_tri_key[k];
+        if (better(t, key.obj, key.id, b)) {
+            b = Closest<R>{t, HIT_TRI, key.id, sc.tri_mat[key.id], key.obj};
+            tl = bvh_tlimit(b.t);
+        }
+    }
+}
+
+// Closest hit through the BVHs: planes and boxes brute force first (their t shortens the walks),
+// then the sphere BVH and the triangle BVH.  Lanes walk their own paths (per-lane node loads); leaf
+// records are contiguous in leaf order.
+template <class R, bool WIDE>
+RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
+    const R tmin = (R)0.001;
+    Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
+    brute_planes_boxes(sc, o, d, tmin, b);
     const BvhRay br = make_bvh_ray(o, d);
     float tl = bvh_tlimit(b.t);
     if (sc.num_sphere_nodes > 0) {
         const R a = dot(d, d);
         FilterRay fr{};
         if constexpr (sizeof(R) == 8) fr = make_filter_ray(o, d);
-        bvh_walk<WIDE>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w, [&](int fc) {
-            const int first = fc >> 4, end = first + (fc & 15);
-            RT_COUNT(w.spheres += end - first);
-            for (int k = first; k < end; ++k) {
-                if constexpr (sizeof(R) == 8)
-                    if (!sphere_filter_pass(sc.bvh_sphere_filter[k], fr)) continue;
-                R t;
-                if (!sphere_candidate(sc.bvh_spheres[k], o, d, a, tmin, t)) continue;
-                const PrimKey key = sc.bvh_sphere_key[k];
-                if (better(t, key.obj, key.id, b)) {
-                    b = Closest<R>{t, HIT_SPHERE, key.id, sc.sphere_mat[key.id], key.obj};
-                    tl = bvh_tlimit(b.t);
-                }
-            }
-        });
+        bvh_walk<WIDE>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w,
+                       [&](int fc) { sphere_leaf(sc, fc, o, d, a, fr, tmin, b, tl, w); });
     }
     if (sc.num_tri_nodes > 0) {
-        bvh_walk<WIDE>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, [&](int fc) {
-            const int first = fc >> 4, end = first + (fc & 15);
-            RT_COUNT(w.tris += end - first);
-            for (int k = first; k < end; ++k) {
-                R t;
-                if (!triangle_candidate(sc.bvh_tris[k], o, d, tmin, t)) continue;
-                const PrimKey key = sc.bvh_tri_key[k];
-                if (better(t, key.obj, key.id, b)) {
-                    b = Closest<R>{t, HIT_TRI, key.id, sc.tri_mat[key.id], key.obj};
-                    tl = bvh_tlimit(b.t);
-                }
-            }
-        });
+        bvh_walk<WIDE>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w,
+                       [&](int fc) { tri_leaf(sc, fc, o, d, tmin, b, tl, w); });
     }
     return b;
 }

@@ -107,6 +107,35 @@ RT_HD bool scatter(const MatRec<R>& m, const Hit<R>& h, V3<R> d, Rng<R>& g, V3<R
 
 struct PixelResult { uint32_t segments, draws; Work work; uint64_t cyc[3]; };
 
+// Shade the segment whose closest hit is c (rayColor's body after world.hit, ray-tracer.js:106-122):
+// emission / scatter / background.  Returns true when the sample's path ended; its radiance L is
+// then in `L`, otherwise (o, d, T, depth) describe the next segment.
+template <class R>
+RT_HD bool shade_segment(const SceneView<R>& sc, const Closest<R>& c, V3<R>& o, V3<R>& d, V3<R>& T, int& depth,
+                         Rng<R>& g, V3<R>& L) {
+    bool done = true;
+    L = mk<R>(0, 0, 0);
+    if (c.kind != HIT_NONE) {
+        const Hit<R> h = hit_record(sc, o, d, c);
+        const MatRec<R> m = sc.mats[h.mat];
+        if (m.type == 3) {                                                    // Emissive (materials.js:87-96)
+            L = mk(T.x * m.emit[0], T.y * m.emit[1], T.z * m.emit[2]);
+        } else {
+            V3<R> nd, att;
+            if (scatter(m, h, d, g, nd, att)) {
+                T = mk(T.x * att.x, T.y * att.y, T.z * att.z);
+                o = h.p;
+                d = nd;
+                done = --depth <= 0;                                          // rayColor(.., 0) returns 0
+            }
+        }
+    } else {
+        const V3<R> bg = background(sc, d);                                   // world.background(ray)
+        L = mk(T.x * bg.x, T.y * bg.y, T.z * bg.z);
+    }
+    return done;
+}
+
 // Trace samples [im.s_begin, s_end) of crop pixel (cx, cy), adding radiance into sum[0..2].
 template <class R, bool COUNT, int ACC = ACC_BRUTE>
 RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int cx, int cy, int s_end, double* sum,
@@ -126,26 +155,8 @@ RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int
         const uint64_t t1 = RT_TICK();
         if (RT_PROFILE) res.cyc[0] += t1 - t0;
         ++res.segments;
-        bool done = true;
-        V3<R> L = mk<R>(0, 0, 0);
-        if (c.kind != HIT_NONE) {
-            const Hit<R> h = hit_record(sc, o, d, c);
-            const MatRec<R> m = sc.mats[h.mat];
-            if (m.type == 3) {                                                // Emissive (materials.js:87-96)
-                L = mk(T.x * m.emit[0], T.y * m.emit[1], T.z * m.emit[2]);
-            } else {
-                V3<R> nd, att;
-                if (scatter(m, h, d, g, nd, att)) {
-                    T = mk(T.x * att.x, T.y * att.y, T.z * att.z);
-                    o = h.p;
-                    d = nd;
-                    done = --depth <= 0;                                      // rayColor(.., 0) returns 0
-                }
-            }
-        } else {
-            V3<R> bg = background(sc, d);                                     // world.background(ray)
-            L = mk(T.x * bg.x, T.y * bg.y, T.z * bg.z);
-        }
+        V3<R> L;
+        const bool done = shade_segment(sc, c, o, d, T, depth, g, L);
         const uint64_t t2 = RT_TICK();
         if (RT_PROFILE) res.cyc[1] += t2 - t1;
         if (done) {

@@ -6,6 +6,7 @@
 // every lane in lockstep, so all record loads are wave-uniform scalar loads; the per-pixel sums are
 // read and written once per launch.
 #include <cstdlib>
+#include <cstring>
 
 #include "pt_launch.h"
 
@@ -40,8 +41,8 @@ void trace_kernel(const TraceArgs<R> args) {
     const ImageParams& im = args.im;
     LdsSpheres lds{nullptr};
     BvhStack stk{nullptr, 0};
-    if constexpr (ACC == ACC_BVH_STACK) {
-        // per-lane traversal stacks, entry k of thread t at [k * 256 + t] (32 KB per workgroup)
+    if constexpr (ACC >= ACC_BVH_STACK) {
+        // per-lane traversal stacks, entry k of thread t at [k * 256 + t] (24 KB per workgroup)
         __shared__ int bvh_stack[RT_BVH_STACK * 256];
         stk.base = bvh_stack + threadIdx.x;
         stk.stride = 256;
@@ -84,6 +85,12 @@ void trace_kernel(const TraceArgs<R> args) {
                 for (int off = 32; off > 0; off >>= 1) v = max(v, (unsigned long long)__shfl_xor(v, off));
                 if (lane == 0) atomicAdd(args.c.totals + 4 + k, v);
             }
+            const uint32_t trips[2] = {r.work.lane_trips, r.work.wave_trips};
+            for (int k = 0; k < 2; ++k) {
+                unsigned long long v = trips[k];
+                for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+                if (lane == 0) atomicAdd(args.c.totals + 7 + k, v);
+            }
         }
     }
 }
@@ -99,14 +106,14 @@ static int sphere_path_override() {
     return v;
 }
 
-// RT_BVH_WALK=skip selects the stackless preorder walk instead of the ordered stack walk (A/B runs)
-static bool bvh_stackless() {
+// RT_BVH_WALK=skip (A/B runs) selects the stackless preorder walk; default: the ordered stack walk
+static int bvh_walk_mode() {
     static int v = -1;
     if (v == -1) {
         const char* e = getenv("RT_BVH_WALK");
-        v = e && e[0] == 's' && e[1] == 'k';
+        v = e && !strncmp(e, "skip", 4) ? ACC_BVH : ACC_BVH_STACK;
     }
-    return v == 1;
+    return v;
 }
 
 template <class R, int ACC>
@@ -123,7 +130,8 @@ hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Cou
     TraceArgs<R> a{sc, im, c};
     const bool count = c.segs || c.draws;
     if (bvh) {
-        if (bvh_stackless()) launch_acc<R, ACC_BVH>(a, tiles, 0, count, stream);
+        const int mode = bvh_walk_mode();
+        if (mode == ACC_BVH) launch_acc<R, ACC_BVH>(a, tiles, 0, count, stream);
         else launch_acc<R, ACC_BVH_STACK>(a, tiles, 0, count, stream);
         return hipGetLastError();
     }
