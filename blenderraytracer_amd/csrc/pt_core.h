@@ -29,11 +29,12 @@ RT_HD uint32_t sample_key(uint32_t pkey, uint32_t sample) {
 template <class R>
 struct Rng {
     uint32_t key, k;
-    RT_HD R next() {
+    RT_HD uint32_t next_u24() {                       // next() == next_u24() * 2^-24
         uint32_t h = lowbias32(key ^ (k * 0x9E3779B9U));
         ++k;
-        return (R)(h >> 8) * (R)(1.0 / 16777216.0);   // exact in f32 and f64
+        return h >> 8;
     }
+    RT_HD R next() { return (R)next_u24() * (R)(1.0 / 16777216.0); }   // exact in f32 and f64
 };
 
 // ---- JS semantics helpers ----------------------------------------------------------------------
@@ -663,22 +664,27 @@ RT_HD Hit<R> hit_record(const SceneView<R>& sc, V3<R> o, V3<R> d, const Closest<
 
 template <class R>
 RT_HD V3<R> random_in_unit_sphere(Rng<R>& g) {                  // math.js:22-26
-    V3<R> p;
+    // A draw is u * 2^-24 (u a 24-bit integer), so 2r - 1 = (u - 2^23) * 2^-23 exactly, and
+    // lengthSquared() of such a point is EXACT in binary64 (squares < 2^-46 granularity, sum < 3):
+    // the binary64 test p.lengthSquared() < 1 is the integer test X^2 + Y^2 + Z^2 < 2^46 — the same
+    // decisions at integer cost (and the exact decision in f32 mode too).
+    int64_t x, y, z;
     do {
-        R a = g.next(), b = g.next(), c = g.next();
-        p = mk(a * (R)2 - (R)1, b * (R)2 - (R)1, c * (R)2 - (R)1);
-    } while (dot(p, p) >= (R)1);
-    return p;
+        x = (int64_t)g.next_u24() - (1 << 23);
+        y = (int64_t)g.next_u24() - (1 << 23);
+        z = (int64_t)g.next_u24() - (1 << 23);
+    } while (x * x + y * y + z * z >= ((int64_t)1 << 46));
+    return mk((R)x * (R)0x1p-23, (R)y * (R)0x1p-23, (R)z * (R)0x1p-23);
 }
 
 template <class R>
 RT_HD V3<R> random_in_unit_disk(Rng<R>& g) {                    // math.js:27-31
-    R x, y;
+    int64_t x, y;                                                 // exact, as random_in_unit_sphere
     do {
-        x = g.next() * (R)2 - (R)1;
-        y = g.next() * (R)2 - (R)1;
-    } while (x * x + y * y + (R)0 * (R)0 >= (R)1);
-    return mk<R>(x, y, 0);
+        x = (int64_t)g.next_u24() - (1 << 23);
+        y = (int64_t)g.next_u24() - (1 << 23);
+    } while (x * x + y * y >= ((int64_t)1 << 46));
+    return mk<R>((R)x * (R)0x1p-23, (R)y * (R)0x1p-23, 0);
 }
 
 // ---- backgrounds (world.js:35-110, Perlin noise.js:29-61) ---------------------------------------
