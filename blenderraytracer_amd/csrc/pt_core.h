@@ -86,6 +86,16 @@ struct PrimKey { int id, obj; };   // index into the World-order arrays, World.o
 // Bounds interleaved by child (lo[axis][child]) so both children's planes of an axis form one float2:
 // the slab test is 6 packed FMAs (v_pk_fma_f32) per node.
 struct Bvh2Node { float lo[3][2]; float hi[3][2]; int child[2]; int pad[2]; };
+// Four-child node (128 B), collapsed from the binary tree: children in pairs (0,1), (2,3) for the
+// packed slab test; child RT_CHILD_EMPTY never hits.  Stack bound checked at build (scene_pack.h).
+struct Bvh4Node { float lo[3][4]; float hi[3][4]; int child[4]; int pad[4]; };
+#define RT_CHILD_EMPTY ((int)0x80000000)
+#ifndef RT_BVH4_STACK
+#define RT_BVH4_STACK 36          // 36 KB of LDS per workgroup (mesh50k needs 35)
+#endif
+#ifndef RT_BVH4_SORT
+#define RT_BVH4_SORT 1            // 1: hit children fully sorted by entry distance; 0: nearest only
+#endif
 #ifndef RT_BVH_STACK
 #define RT_BVH_STACK 24           // 24 KB of LDS per 256-lane workgroup; trees up to ~16.7M primitives
 #endif
@@ -125,6 +135,8 @@ struct SceneView {
     const Bvh2Node* sphere_wide;   // two-child nodes of the two trees (preorder)
     const Bvh2Node* tri_wide;
     int num_sphere_wide, num_tri_wide;
+    const Bvh4Node* sphere_wide4;  // four-child collapse of the two trees (preorder)
+    const Bvh4Node* tri_wide4;
     // camera (camera.js:8-36 vectors, computed on the host in binary64)
     R cam_o[3], cam_llc[3], cam_h[3], cam_v[3], cam_u[3], cam_vv[3], cam_w[3];
     R lens_radius;
@@ -591,7 +603,72 @@ RT_HD void tri_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R tmin, Cl
 // Closest hit through the BVHs: planes and boxes brute force first (their t shortens the walks),
 // then the sphere BVH and the triangle BVH.  Lanes walk their own paths (per-lane node loads); leaf
 // records are contiguous in leaf order.
-template <class R, bool WIDE>
+// Four children at once: entry distance and hit flag per child (pairs (0,1), (2,3) as packed FMAs).
+RT_HD void bvh_node4_hit(const Bvh4Node& n, const BvhRay& r, float tlimit, float tn[4], bool hit[4]) {
+    for (int p = 0; p < 4; p += 2) {
+        rt_f2 a[3], b[3];
+        for (int k = 0; k < 3; ++k) {
+            const rt_f2 inv = {r.inv[k], r.inv[k]};
+            const rt_f2 slo = {-r.slo[k], -r.slo[k]}, shi = {-r.shi[k], -r.shi[k]};
+            a[k] = __builtin_elementwise_fma(rt_f2{n.lo[k][p], n.lo[k][p + 1]}, inv, slo);
+            b[k] = __builtin_elementwise_fma(rt_f2{n.hi[k][p], n.hi[k][p + 1]}, inv, shi);
+        }
+        tn[p] = fmaxf(fmaxf(fminf(a[0].x, b[0].x), fminf(a[1].x, b[1].x)), fmaxf(fminf(a[2].x, b[2].x), 0.0f));
+        tn[p + 1] = fmaxf(fmaxf(fminf(a[0].y, b[0].y), fminf(a[1].y, b[1].y)), fmaxf(fminf(a[2].y, b[2].y), 0.0f));
+        const float f0 = fminf(fminf(fmaxf(a[0].x, b[0].x), fmaxf(a[1].x, b[1].x)), fminf(fmaxf(a[2].x, b[2].x), tlimit));
+        const float f1 = fminf(fminf(fmaxf(a[0].y, b[0].y), fmaxf(a[1].y, b[1].y)), fminf(fmaxf(a[2].y, b[2].y), tlimit));
+        hit[p] = tn[p] <= f0 && n.child[p] != RT_CHILD_EMPTY;
+        hit[p + 1] = tn[p + 1] <= f1 && n.child[p + 1] != RT_CHILD_EMPTY;
+    }
+}
+
+// Ordered walk over four-child nodes: the hit children sorted by entry distance (a 5-exchange
+// network on (distance, child) with misses as (+inf, EMPTY)), the nearest taken, the others pushed
+// farthest first.  Every hit child is visited (a child whose f32 entry distance overflowed to +inf
+// sorts among the misses but keeps its reference), so culling stays exactly that of the slab test.
+template <class Leaf>
+RT_HD void bvh_walk4(const Bvh4Node* nodes, const BvhRay& br, const float& tl, BvhStack stk, Work& w, Leaf&& leaf) {
+    int sp = 0, cur = 0;
+    for (;;) {
+        if (cur >= 0) {
+            const Bvh4Node n = nodes[cur];
+            RT_COUNT(++w.nodes);
+            float key[4];
+            bool hit[4];
+            bvh_node4_hit(n, br, tl, key, hit);
+            int c[4];
+            for (int k = 0; k < 4; ++k) {
+                c[k] = hit[k] ? n.child[k] : RT_CHILD_EMPTY;
+                key[k] = hit[k] ? key[k] : INFINITY;
+            }
+            auto cx = [&](int i, int j) {
+                if (key[j] < key[i]) {
+                    const float tk = key[i]; key[i] = key[j]; key[j] = tk;
+                    const int tc = c[i]; c[i] = c[j]; c[j] = tc;
+                }
+            };
+#if RT_BVH4_SORT
+            cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
+#else
+            cx(0, 1); cx(2, 3); cx(0, 2);          // nearest first; the rest pushed unordered
+#endif
+            for (int k = 3; k >= 1; --k)
+                if (c[k] != RT_CHILD_EMPTY) stk.base[(sp++) * stk.stride] = c[k];
+            if (c[0] != RT_CHILD_EMPTY) {
+                cur = c[0];
+                continue;
+            }
+        } else {
+            leaf(~cur);
+        }
+        if (sp == 0) break;
+        cur = stk.base[(--sp) * stk.stride];
+    }
+}
+
+// WALK: 0 = stackless preorder (BvhNode), 1 = ordered two-child (Bvh2Node), 2 = ordered four-child
+// (Bvh4Node)
+template <class R, int WALK>
 RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
     const R tmin = (R)0.001;
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
@@ -602,24 +679,27 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
         const R a = dot(d, d);
         FilterRay fr{};
         if constexpr (sizeof(R) == 8) fr = make_filter_ray(o, d);
-        bvh_walk<WIDE>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w,
-                       [&](int fc) { sphere_leaf(sc, fc, o, d, a, fr, tmin, b, tl, w); });
+        auto leaf = [&](int fc) { sphere_leaf(sc, fc, o, d, a, fr, tmin, b, tl, w); };
+        if constexpr (WALK == 2) bvh_walk4(sc.sphere_wide4, br, tl, stk, w, leaf);
+        else bvh_walk<WALK == 1>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w, leaf);
     }
     if (sc.num_tri_nodes > 0) {
-        bvh_walk<WIDE>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w,
-                       [&](int fc) { tri_leaf(sc, fc, o, d, tmin, b, tl, w); });
+        auto leaf = [&](int fc) { tri_leaf(sc, fc, o, d, tmin, b, tl, w); };
+        if constexpr (WALK == 2) bvh_walk4(sc.tri_wide4, br, tl, stk, w, leaf);
+        else bvh_walk<WALK == 1>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, leaf);
     }
     return b;
 }
 
 // acceleration modes of the trace kernel
-enum Accel : int { ACC_BRUTE = 0, ACC_LDS = 1, ACC_BVH = 2, ACC_BVH_STACK = 3 };
+enum Accel : int { ACC_BRUTE = 0, ACC_LDS = 1, ACC_BVH = 2, ACC_BVH_STACK = 3, ACC_BVH4 = 4 };
 
 template <class R, int ACC>
 RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, const LdsSpheres lds, Work& w,
                                  BvhStack stk) {
-    if constexpr (ACC == ACC_BVH) return closest_hit_bvh<R, false>(sc, o, d, w, stk);
-    else if constexpr (ACC == ACC_BVH_STACK) return closest_hit_bvh<R, true>(sc, o, d, w, stk);
+    if constexpr (ACC == ACC_BVH) return closest_hit_bvh<R, 0>(sc, o, d, w, stk);
+    else if constexpr (ACC == ACC_BVH_STACK) return closest_hit_bvh<R, 1>(sc, o, d, w, stk);
+    else if constexpr (ACC == ACC_BVH4) return closest_hit_bvh<R, 2>(sc, o, d, w, stk);
     else return closest_hit<R, ACC == ACC_LDS>(sc, o, d, lds);
 }
 

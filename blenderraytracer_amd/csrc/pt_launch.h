@@ -15,7 +15,8 @@ struct Counters {
 };
 
 template <class R>
-hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh, hipStream_t stream);
+// walk: ACC_BRUTE (World order), ACC_BVH_STACK (two-child BVH walk) or ACC_BVH4 (four-child walk)
+hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, int walk, hipStream_t stream);
 
 struct FinalizeParams {
     int n;

@@ -101,13 +101,14 @@ struct DeviceScene {
     DevBuf<PrimKey> bvh_sphere_key, bvh_tri_key;
     DevBuf<TriRec<R>> bvh_tris;
     DevBuf<Bvh2Node> sphere_wide, tri_wide;
+    DevBuf<Bvh4Node> sphere_wide4, tri_wide4;
     SceneView<R> view{};
     void release() {
         runs.release(); spheres.release(); sphere_filter.release(); sphere_r.release(); planes.release(); boxes.release(); tris.release();
         sphere_mat.release(); plane_mat.release(); box_mat.release(); tri_mat.release(); perm.release(); mats.release();
         plane_obj.release(); box_obj.release(); sphere_nodes.release(); tri_nodes.release(); bvh_spheres.release();
         bvh_sphere_filter.release(); bvh_sphere_key.release(); bvh_tri_key.release(); bvh_tris.release();
-        sphere_wide.release(); tri_wide.release();
+        sphere_wide.release(); tri_wide.release(); sphere_wide4.release(); tri_wide4.release();
     }
 };
 
@@ -123,6 +124,7 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     UP(plane_obj, hs.plane_obj); UP(box_obj, hs.box_obj); UP(sphere_nodes, hs.sphere_bvh); UP(tri_nodes, hs.tri_bvh);
     UP(bvh_spheres, rec.bvh_spheres); UP(bvh_sphere_filter, rec.bvh_sphere_filter); UP(bvh_sphere_key, rec.bvh_sphere_key);
     UP(bvh_tri_key, rec.bvh_tri_key); UP(bvh_tris, rec.bvh_tris); UP(sphere_wide, hs.sphere_wide); UP(tri_wide, hs.tri_wide);
+    UP(sphere_wide4, hs.sphere_wide4); UP(tri_wide4, hs.tri_wide4);
 #undef UP
     if (e != hipSuccess) return fail(RT_ERR_DEVICE, "scene upload: %s", hipGetErrorString(e));
     SceneView<R>& v = ds.view;
@@ -134,6 +136,7 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     v.bvh_spheres = ds.bvh_spheres.p; v.bvh_sphere_filter = ds.bvh_sphere_filter.p; v.bvh_sphere_key = ds.bvh_sphere_key.p;
     v.bvh_tris = ds.bvh_tris.p; v.bvh_tri_key = ds.bvh_tri_key.p;
     v.sphere_wide = ds.sphere_wide.p; v.tri_wide = ds.tri_wide.p;
+    v.sphere_wide4 = ds.sphere_wide4.p; v.tri_wide4 = ds.tri_wide4.p;
     fill_view_constants(v, hs, d);
     return RT_OK;
 }
@@ -152,6 +155,7 @@ struct rt_scene {
     int num_prims = 0;
     int bvh_prims = 0;              // spheres + triangles (the primitives the BVHs cover)
     bool bvh_ok = true;             // both trees fit the traversal stack (depth <= RT_BVH_STACK)
+    bool bvh4_ok = true;            // the four-child walk's stack bound fits RT_BVH4_STACK
     double record_bytes = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {};
@@ -227,9 +231,9 @@ int check_accel(const rt_scene* sc, const rt_settings* s) {
 
 hipError_t trace(rt_scene* sc, const rt_settings* s, const ImageParams& im, const Counters& c, hipStream_t st) {
     if (im.max_depth <= 0) return hipSuccess;   // rayColor(ray, depth<=0) is 0: nothing to trace
-    const bool bvh = use_bvh(sc, s);
-    if (s->precision == RT_PREC_F32) return launch_trace<float>(sc->s32.view, im, c, bvh, st);
-    return launch_trace<double>(sc->s64.view, im, c, bvh, st);
+    const int walk = !use_bvh(sc, s) ? ACC_BRUTE : (sc->bvh4_ok ? ACC_BVH4 : ACC_BVH_STACK);
+    if (s->precision == RT_PREC_F32) return launch_trace<float>(sc->s32.view, im, c, walk, st);
+    return launch_trace<double>(sc->s64.view, im, c, walk, st);
 }
 
 // totals = [segments, BVH nodes, sphere tests, triangle tests] of the launches
@@ -299,6 +303,7 @@ int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out) {
     sc->num_prims = hs.num_prims;
     sc->bvh_prims = (int)(hs.sphere_r.size() + hs.tri_mat.size());
     sc->bvh_ok = hs.bvh_depth <= RT_BVH_STACK;
+    sc->bvh4_ok = sc->bvh_ok && hs.bvh4_stack <= RT_BVH4_STACK;
     sc->record_bytes = hs.record_bytes;
     if ((rc = build_device(sc->s64, hs, *desc)) || (rc = build_device(sc->s32, hs, *desc))) {
         rt_scene_destroy(sc);

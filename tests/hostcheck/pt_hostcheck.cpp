@@ -30,8 +30,9 @@ struct HostView {
         v.bvh_spheres = rec.bvh_spheres.data(); v.bvh_sphere_filter = rec.bvh_sphere_filter.data();
         v.bvh_sphere_key = rec.bvh_sphere_key.data(); v.bvh_tris = rec.bvh_tris.data(); v.bvh_tri_key = rec.bvh_tri_key.data();
         v.sphere_wide = hs.sphere_wide.data(); v.tri_wide = hs.tri_wide.data();
+        v.sphere_wide4 = hs.sphere_wide4.data(); v.tri_wide4 = hs.tri_wide4.data();
         fill_view_constants(v, hs, *d);
-        return true;
+        return hs.bvh4_stack <= 64;                  // the host walks use 64-entry stacks
     }
 };
 
@@ -51,7 +52,7 @@ static int render(const rt_scene_desc* d, const rt_settings* s, double* sum, uin
     im.max_depth = s->max_depth;
     im.aa_mode = s->aa_mode;
     im.seedm = host_seed_mix(s->seed);
-    int stack[RT_BVH_STACK];
+    int stack[64];
     const BvhStack stk{stack, 1};
     const LdsSpheres no_lds{nullptr};
     for (int cy = 0; cy < im.ch; ++cy)
@@ -59,10 +60,12 @@ static int render(const rt_scene_desc* d, const rt_settings* s, double* sum, uin
             const size_t q = (size_t)cy * im.cw + cx;
             PixelResult r{0, 0, {0, 0, 0}};
             double* acc = sum + 3 * q;
-            // accel: RT_ACCEL_BVH = the ordered stack walk the library runs, 3 = the stackless walk
+            // accel: RT_ACCEL_BVH = the four-child walk; hostcheck-only selectors 3 = the stackless
+            // walk, 4 = the two-child walk
             if (im.max_depth > 0)
-                r = s->accel == RT_ACCEL_BVH ? trace_pixel<R, true, ACC_BVH_STACK>(v, im, cx, cy, im.s_end, acc, no_lds, stk)
+                r = s->accel == RT_ACCEL_BVH ? trace_pixel<R, true, ACC_BVH4>(v, im, cx, cy, im.s_end, acc, no_lds, stk)
                   : s->accel == 3            ? trace_pixel<R, true, ACC_BVH>(v, im, cx, cy, im.s_end, acc)
+                  : s->accel == 4            ? trace_pixel<R, true, ACC_BVH_STACK>(v, im, cx, cy, im.s_end, acc, no_lds, stk)
                                              : trace_pixel<R, true, ACC_BRUTE>(v, im, cx, cy, im.s_end, acc);
             segs[q] = r.segments;
             draws[q] = r.draws;
@@ -182,10 +185,12 @@ extern "C" long long ptc_bvh_check(const rt_scene_desc* d, long long n, unsigned
         const Closest<double> a = closest_hit<double, false>(v, O, D);
         Work w{0, 0, 0};
         int stack[RT_BVH_STACK];
-        const Closest<double> b = closest_hit_bvh<double, false>(v, O, D, w, BvhStack{nullptr, 0});
-        const Closest<double> c = closest_hit_bvh<double, true>(v, O, D, w, BvhStack{stack, 1});
+        int stack4[64];
+        const Closest<double> b = closest_hit_bvh<double, 0>(v, O, D, w, BvhStack{nullptr, 0});
+        const Closest<double> c = closest_hit_bvh<double, 1>(v, O, D, w, BvhStack{stack, 1});
+        const Closest<double> e = closest_hit_bvh<double, 2>(v, O, D, w, BvhStack{stack4, 1});
         if (a.kind != HIT_NONE) ++nh;
-        for (const Closest<double>& x : {b, c}) {
+        for (const Closest<double>& x : {b, c, e}) {
             const bool same = a.kind == x.kind && (a.kind == HIT_NONE || (a.idx == x.idx && a.mat == x.mat &&
                                                                          std::memcmp(&a.t, &x.t, 8) == 0));
             bad += !same;
@@ -193,4 +198,15 @@ extern "C" long long ptc_bvh_check(const rt_scene_desc* d, long long n, unsigned
     }
     if (hits) *hits = nh;
     return bad;
+}
+
+// BVH shape: deepest leaf of the binary trees and the four-child walk's worst stack use
+extern "C" int ptc_bvh_info(const rt_scene_desc* d, int* depth, int* stack4, int* nodes2, int* nodes4) {
+    HostView<double> hv;
+    hv.init(d);
+    *depth = hv.hs.bvh_depth;
+    *stack4 = hv.hs.bvh4_stack;
+    *nodes2 = (int)(hv.hs.sphere_wide.size() + hv.hs.tri_wide.size());
+    *nodes4 = (int)(hv.hs.sphere_wide4.size() + hv.hs.tri_wide4.size());
+    return 0;
 }

@@ -42,13 +42,13 @@ def test_kernel_logic_f32_close_to_oracle():
     assert np.sqrt(np.mean((r["mean"] - o["mean"]) ** 2)) < 0.05
 
 
-@pytest.mark.parametrize("walk", ["stack", "stackless"])
+@pytest.mark.parametrize("walk", ["four-child", "two-child", "stackless"])
 @pytest.mark.parametrize("case", gc.case_names())
 def test_kernel_logic_bvh_matches_reference(case, walk):
-    """RT_ACCEL_BVH (closest_hit_bvh, ordered stack walk and stackless walk) gives the same decisions
-    as World.hit on every golden case."""
+    """RT_ACCEL_BVH (closest_hit_bvh: the ordered four- and two-child walks and the stackless walk)
+    gives the same decisions as World.hit on every golden case."""
     rt, c = gc.tracer_for(case)
-    rt.accel = capi.RT_ACCEL_BVH if walk == "stack" else 3     # 3: hostcheck-only stackless selector
+    rt.accel = {"four-child": capi.RT_ACCEL_BVH, "stackless": 3, "two-child": 4}[walk]   # 3, 4: hostcheck-only
     r = hb.render(rt.packed(), rt.settings(crop=c["crop"]))
     assert np.array_equal(r["segments"], gc.load_array(case, "segs"))
     assert np.array_equal(r["draws"], gc.load_array(case, "draws"))
