@@ -213,3 +213,43 @@ def test_checkpoint_resume_is_bit_exact(gpu):
     s2, d2 = rt2.checkpoint()
     assert d2 == 10
     rt2.close()
+
+
+_WALK_SCRIPT = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import torch  # noqa: F401  (HIP runtime first)
+from blenderraytracer_amd import capi
+from blenderraytracer_amd.renderer import GpuRayTracer
+from blenderraytracer_amd.scene import load_scene_json
+out = {}
+for name, w, h, crop in (("mesh50k", 1920, 1080, (900, 480, 64, 48)), ("kitchen_sink.json", 96, 64, None),
+                         ("rtow.json", 160, 90, None)):
+    rt = GpuRayTracer(w, h, seed=9, accel=capi.RT_ACCEL_BVH)
+    assert rt.load_from_json(load_scene_json(name))
+    rt.update_render_settings({"samples": 4, "maxBounces": 5})
+    r = rt.render(crop=crop, want=("mean", "segments", "draws"))
+    for k in ("mean", "segments", "draws"):
+        out[f"{name}.{k}"] = r[k]
+np.savez(sys.argv[2], **out)
+'''
+
+
+@pytest.mark.parametrize("walk", ["four", "skip"])
+def test_alternative_bvh_walks_bit_identical(gpu, tmp_path, walk):
+    """The A/B walks (RT_BVH_WALK=four: four-child nodes; skip: stackless preorder) render the same
+    bits as the default two-child walk (run in child processes: the walk is chosen per process)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for mode in ("two", walk):
+        f = tmp_path / f"{mode}.npz"
+        env = dict(os.environ, RT_BVH_WALK=mode)
+        r = subprocess.run([sys.executable, "-c", _WALK_SCRIPT, root, str(f)], env=env, capture_output=True,
+                           text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res[mode] = np.load(f)
+    for k in res["two"].files:
+        assert np.array_equal(res["two"][k], res[walk][k], equal_nan=True), k
