@@ -1,10 +1,11 @@
 // pt_trace.hip — the path-tracing megakernel and its epilogue for gfx950 (MI355X).
 //
 // One lane owns one pixel of the crop window and traces that pixel's samples [s_begin, s_end) in
-// order (trace_pixel, pt_path.h).  A 256-thread workgroup covers a 16x16 tile, each wave an 8x8
-// block, so neighbouring rays share a wave.  Primitive records are walked in World.objects order by
-// every lane in lockstep, so all record loads are wave-uniform scalar loads; the per-pixel sums are
-// read and written once per launch.
+// order (trace_pixel, pt_path.h).  Each wave covers an 8x8 pixel block, so neighbouring rays share a
+// wave.  BVH mode: every lane walks its own path through the two-child BVH with a per-lane stack in
+// LDS; brute-force mode: primitive records are walked in World.objects order by every lane in
+// lockstep, so all record loads are wave-uniform scalar loads.  The per-pixel sums are read and
+// written once per launch.
 #include <cstdlib>
 #include <cstring>
 
@@ -18,6 +19,16 @@ struct TraceArgs {
     ImageParams im;
     Counters c;
 };
+
+// Workgroup = RT_WG_WAVES waves, each an 8x8 pixel block; tiles of 8x8 (1 wave), 16x8 (2) or 16x16 (4).
+// One-wave workgroups measured fastest (RTOW f64 4350 vs 4190 Msamples/s, mesh50k 3342 vs 3094): 4x
+// more, smaller work items shorten the tail of a frame whose pixels cost very different amounts.
+#ifndef RT_WG_WAVES
+#define RT_WG_WAVES 1
+#endif
+constexpr int kWgThreads = 64 * RT_WG_WAVES;
+constexpr int kTileW = RT_WG_WAVES >= 2 ? 16 : 8;
+constexpr int kTileH = RT_WG_WAVES == 4 ? 16 : 8;
 
 #ifndef RT_MIN_WAVES_PER_SIMD
 #define RT_MIN_WAVES_PER_SIMD 8   // 64 VGPRs: latency-bound loop, 8 waves/SIMD measured fastest
@@ -36,16 +47,16 @@ constexpr int waves_per_simd() {
 }
 
 template <class R, bool COUNT, int ACC>
-__global__ __launch_bounds__(256, (waves_per_simd<R, ACC>()))
+__global__ __launch_bounds__(kWgThreads, (waves_per_simd<R, ACC>()))
 void trace_kernel(const TraceArgs<R> args) {
     const ImageParams& im = args.im;
     LdsSpheres lds{nullptr};
     BvhStack stk{nullptr, 0};
     if constexpr (ACC >= ACC_BVH_STACK) {
-        // per-lane traversal stacks, entry k of thread t at [k * 256 + t] (24 / 36 KB per workgroup)
-        __shared__ int bvh_stack[(ACC == ACC_BVH4 ? RT_BVH4_STACK : RT_BVH_STACK) * 256];
+        // per-lane traversal stacks, entry k of thread t at [k * kWgThreads + t] (96 / 144 B per lane)
+        __shared__ int bvh_stack[(ACC == ACC_BVH4 ? RT_BVH4_STACK : RT_BVH_STACK) * kWgThreads];
         stk.base = bvh_stack + threadIdx.x;
-        stk.stride = 256;
+        stk.stride = kWgThreads;
     }
     if constexpr (ACC == ACC_LDS) {
         // stage the binary32 sphere filter records of the whole scene in LDS (one copy per workgroup)
@@ -55,10 +66,10 @@ void trace_kernel(const TraceArgs<R> args) {
         lds = LdsSpheres{lds_spheres};
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int tiles_x = (im.cw + 15) >> 4;
+    const int tiles_x = (im.cw + kTileW - 1) / kTileW;
     const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
-    const int cx = tx * 16 + (wave & 1) * 8 + (lane & 7);                    // 8x8 pixels per wave
-    const int cy = ty * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int cx = tx * kTileW + (wave % (kTileW / 8)) * 8 + (lane & 7);     // 8x8 pixels per wave
+    const int cy = ty * kTileH + (wave / (kTileW / 8)) * 8 + (lane >> 3);
     const bool valid = cx < im.cw && cy < im.ch;
     const size_t q = (size_t)cy * im.cw + cx;
     double acc[3] = {0, 0, 0};
@@ -120,15 +131,15 @@ static int bvh_walk_mode(int four_ok) {
 
 template <class R, int ACC>
 static void launch_acc(const TraceArgs<R>& a, int tiles, size_t lds_bytes, bool count, hipStream_t stream) {
-    if (count) hipLaunchKernelGGL((trace_kernel<R, true, ACC>), dim3(tiles), dim3(256), lds_bytes, stream, a);
-    else hipLaunchKernelGGL((trace_kernel<R, false, ACC>), dim3(tiles), dim3(256), lds_bytes, stream, a);
+    if (count) hipLaunchKernelGGL((trace_kernel<R, true, ACC>), dim3(tiles), dim3(kWgThreads), lds_bytes, stream, a);
+    else hipLaunchKernelGGL((trace_kernel<R, false, ACC>), dim3(tiles), dim3(kWgThreads), lds_bytes, stream, a);
 }
 
 template <class R>
 hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, int walk,
                         hipStream_t stream) {
     if (im.cw <= 0 || im.ch <= 0 || im.s_end <= im.s_begin) return hipSuccess;
-    const int tiles = ((im.cw + 15) >> 4) * ((im.ch + 15) >> 4);
+    const int tiles = ((im.cw + kTileW - 1) / kTileW) * ((im.ch + kTileH - 1) / kTileH);
     TraceArgs<R> a{sc, im, c};
     const bool count = c.segs || c.draws;
     if (walk != ACC_BRUTE) {
