@@ -16,25 +16,41 @@ LIB = os.path.join(HERE, "hostcheck", "_build", "libpt_hostcheck.so")
 _lib = None
 
 
-def build():
-    os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    if os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(d) for d in DEPS):
-        return LIB
+def build(defines=(), name="libpt_hostcheck.so"):
+    target = os.path.join(os.path.dirname(LIB), name)
+    os.makedirs(os.path.dirname(target), exist_ok=True)
+    if os.path.exists(target) and all(os.path.getmtime(target) >= os.path.getmtime(d) for d in DEPS):
+        return target
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     subprocess.check_call([hipcc, "--offload-host-only", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-                           "-I", os.path.join(ROOT, "include"), SRC, "-o", LIB])
-    return LIB
+                           *[f"-D{d}" for d in defines], "-I", os.path.join(ROOT, "include"), SRC, "-o", target])
+    return target
 
 
-def lib():
+def _bind(L):
+    L.ptc_render.argtypes = [C.POINTER(capi.SceneDesc), C.POINTER(capi.Settings), C.POINTER(C.c_double),
+                             C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    L.ptc_bvh_check.argtypes = [C.POINTER(capi.SceneDesc), C.c_longlong, C.c_uint, C.POINTER(C.c_longlong)]
+    L.ptc_bvh_check.restype = C.c_longlong
+    L.ptc_bvh_info.argtypes = [C.POINTER(capi.SceneDesc)] + [C.POINTER(C.c_int)] * 4
+    return L
+
+
+def lib(defines=()):
+    """The hostcheck library; `defines` builds (and caches) a variant with -D flags."""
     global _lib
+    if defines:
+        return _bind(C.CDLL(build(defines, "libpt_hostcheck_%s.so" % "_".join(d.replace("=", "") for d in defines))))
     if _lib is None:
-        _lib = C.CDLL(build())
-        _lib.ptc_render.argtypes = [C.POINTER(capi.SceneDesc), C.POINTER(capi.Settings), C.POINTER(C.c_double),
-                                    C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
-        _lib.ptc_bvh_check.argtypes = [C.POINTER(capi.SceneDesc), C.c_longlong, C.c_uint, C.POINTER(C.c_longlong)]
-        _lib.ptc_bvh_check.restype = C.c_longlong
+        _lib = _bind(C.CDLL(build()))
     return _lib
+
+
+def bvh_info(packed, L=None):
+    """(deepest leaf of the binary trees, four-child walk stack bound, two-child nodes, four-child nodes)"""
+    v = [C.c_int() for _ in range(4)]
+    (L or lib()).ptc_bvh_info(C.byref(packed.desc), *[C.byref(x) for x in v])
+    return tuple(x.value for x in v)
 
 
 def bvh_check(packed, n, seed):
