@@ -12,6 +12,7 @@ struct Counters {
     uint32_t* segs;            // optional n per-pixel world.hit counts
     uint32_t* draws;           // optional n per-pixel RNG draws
     unsigned long long* totals;   // optional [segments, BVH nodes, sphere tests, triangle tests]
+    unsigned long long* queue = nullptr;   // pixel-queue head (RT_PIXEL_QUEUE builds), zeroed per launch
 };
 
 template <class R>

@@ -173,4 +173,86 @@ RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int
     return res;
 }
 
+// Pixel-queue order: 8x8 blocks of the crop in raster order, the 64 pixels of a block consecutive, so
+// a wave's first fetch takes one whole block.  Positions past the crop's right/bottom edge are skipped.
+RT_HD inline uint32_t queue_length(const ImageParams& im) {
+    return (uint32_t)((im.cw + 7) / 8) * (uint32_t)((im.ch + 7) / 8) * 64u;
+}
+RT_HD inline bool queue_pixel(const ImageParams& im, uint32_t p, int& cx, int& cy) {
+    const uint32_t tiles_x = (uint32_t)(im.cw + 7) / 8, t = p >> 6, w = p & 63;
+    cx = (int)((t % tiles_x) * 8 + (w & 7));
+    cy = (int)((t / tiles_x) * 8 + (w >> 3));
+    return cx < im.cw && cy < im.ch;
+}
+
+// Pixel-queue variant of trace_pixel: a lane whose pixel has finished its samples takes the next
+// pixel index from `fetch()` (a wave-aggregated atomic on the GPU) inside the same loop, so no lane
+// idles while another pixel of its wave is still tracing.  Each pixel's samples and results are
+// exactly trace_pixel's (same keys, same order); sum/segs/draws are indexed by crop pixel.
+template <class R, bool COUNT, int ACC, class Fetch>
+RT_HD PixelResult trace_pixels_queue(const SceneView<R>& sc, const ImageParams& im, Fetch&& fetch, double* sum,
+                                     uint32_t* segs, uint32_t* draws, const LdsSpheres lds, BvhStack stk) {
+    PixelResult res{0, 0, {0, 0, 0}, {0, 0, 0}};
+    const uint32_t n = queue_length(im);
+    Rng<R> g;
+    V3<R> o, d, T = mk<R>(1, 1, 1);
+    int depth = im.max_depth, i = 0, j = 0, s = 0;
+    uint32_t pkey = 0, psegs = 0, pdraws = 0;
+    size_t q = 0;
+    double sx = 0, sy = 0, sz = 0;
+    auto next_pixel = [&]() -> bool {
+        for (;;) {
+            const uint32_t p = fetch();
+            if (p >= n) return false;
+            int cx, cy;
+            if (!queue_pixel(im, p, cx, cy)) continue;
+            const int row = im.y0 + cy;
+            i = im.x0 + cx;
+            j = im.height - 1 - row;
+            pkey = pixel_key(im.seedm, (uint32_t)row * (uint32_t)im.width + (uint32_t)i);
+            q = (size_t)cy * im.cw + cx;
+            sx = sum[3 * q]; sy = sum[3 * q + 1]; sz = sum[3 * q + 2];
+            psegs = pdraws = 0;
+            s = im.s_begin;
+            T = mk<R>(1, 1, 1);
+            depth = im.max_depth;
+            start_sample(sc, im, i, j, pkey, s, g, o, d);
+            return true;
+        }
+    };
+    bool live = im.s_begin < im.s_end && next_pixel();
+    while (live) {
+        const uint64_t t0 = RT_TICK();
+        const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, lds, res.work, stk);
+        const uint64_t t1 = RT_TICK();
+        if (RT_PROFILE) res.cyc[0] += t1 - t0;
+        ++psegs;
+        V3<R> L;
+        const bool done = shade_segment(sc, c, o, d, T, depth, g, L);
+        const uint64_t t2 = RT_TICK();
+        if (RT_PROFILE) res.cyc[1] += t2 - t1;
+        if (done) {
+            sx += (double)L.x; sy += (double)L.y; sz += (double)L.z;
+            if (COUNT) pdraws += g.k;
+            ++s;
+            T = mk<R>(1, 1, 1);
+            depth = im.max_depth;
+            if (s < im.s_end) {
+                start_sample(sc, im, i, j, pkey, s, g, o, d);
+            } else {
+                sum[3 * q] = sx; sum[3 * q + 1] = sy; sum[3 * q + 2] = sz;
+                if (COUNT) {
+                    if (segs) segs[q] += psegs;
+                    if (draws) draws[q] += pdraws;
+                }
+                res.segments += psegs;
+                res.draws += pdraws;
+                live = next_pixel();
+            }
+        }
+        if (RT_PROFILE) res.cyc[2] += RT_TICK() - t2;
+    }
+    return res;
+}
+
 }  // namespace rt

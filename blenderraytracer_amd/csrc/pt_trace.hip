@@ -6,6 +6,7 @@
 // LDS; brute-force mode: primitive records are walked in World.objects order by every lane in
 // lockstep, so all record loads are wave-uniform scalar loads.  The per-pixel sums are read and
 // written once per launch.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -41,6 +42,12 @@ constexpr int kTileH = RT_WG_WAVES == 4 ? 16 : 8;
 #define RT_BVH_WAVES_F32 5        // binary32 BVH walk: 96 VGPRs (measured 3/4/5 waves: 5362/5230/5506)
 #endif
 
+// RT_PIXEL_QUEUE=1 (A/B builds): a grid of one resident workgroup per wave slot whose lanes take
+// pixels from a global queue (trace_pixels_queue, pt_path.h) instead of one lane per pixel
+#ifndef RT_PIXEL_QUEUE
+#define RT_PIXEL_QUEUE 0
+#endif
+
 template <class R, int ACC>
 constexpr int waves_per_simd() {
     return ACC >= ACC_BVH ? (sizeof(R) == 8 ? RT_BVH_WAVES_PER_SIMD : RT_BVH_WAVES_F32) : RT_MIN_WAVES_PER_SIMD;
@@ -66,6 +73,19 @@ void trace_kernel(const TraceArgs<R> args) {
         lds = LdsSpheres{lds_spheres};
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#if RT_PIXEL_QUEUE
+    (void)wave;
+    unsigned long long* const head = args.c.queue;
+    auto fetch = [head]() -> uint32_t {             // wave-aggregated: one atomic per fetching wave
+        const uint64_t mask = __ballot(1);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+        uint32_t base = 0;
+        if (rank == 0) base = (uint32_t)atomicAdd(head, (unsigned long long)__popcll(mask));
+        return (uint32_t)__builtin_amdgcn_readfirstlane(base) + rank;
+    };
+    const PixelResult r = trace_pixels_queue<R, COUNT, ACC>(args.sc, im, fetch, args.c.sum, COUNT ? args.c.segs : nullptr,
+                                                            COUNT ? args.c.draws : nullptr, lds, stk);
+#else
     const int tiles_x = (im.cw + kTileW - 1) / kTileW;
     // raster tile order: workgroups are dealt round-robin to the 8 XCDs, so every XCD gets an even mix
     // of cheap (sky) and expensive tiles.  Measured worse: reversed raster (-6 %), scattered (-6 %)
@@ -86,6 +106,7 @@ void trace_kernel(const TraceArgs<R> args) {
             if (args.c.draws) args.c.draws[q] += r.draws;
         }
     }
+#endif
     if (args.c.totals) {
         const uint32_t parts[4] = {r.segments, r.work.nodes, r.work.spheres, r.work.tris};
         for (int k = 0; k < (ACC >= ACC_BVH ? 4 : 1); ++k) {
@@ -132,8 +153,24 @@ static int bvh_walk_mode(int four_ok) {
     return v == ACC_BVH4 && !four_ok ? ACC_BVH_STACK : v;
 }
 
+static int device_cus() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    return cus;
+}
+
 template <class R, int ACC>
 static void launch_acc(const TraceArgs<R>& a, int tiles, size_t lds_bytes, bool count, hipStream_t stream) {
+    if (RT_PIXEL_QUEUE) {
+        // one workgroup per resident wave slot (4 SIMDs per CU), never more than the queue's blocks
+        const int slots = device_cus() * 4 * waves_per_simd<R, ACC>() / RT_WG_WAVES;
+        tiles = (int)std::min<uint32_t>((uint32_t)slots, (queue_length(a.im) / 64 + RT_WG_WAVES - 1) / RT_WG_WAVES);
+    }
     if (count) hipLaunchKernelGGL((trace_kernel<R, true, ACC>), dim3(tiles), dim3(kWgThreads), lds_bytes, stream, a);
     else hipLaunchKernelGGL((trace_kernel<R, false, ACC>), dim3(tiles), dim3(kWgThreads), lds_bytes, stream, a);
 }
@@ -145,6 +182,11 @@ hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Cou
     const int tiles = ((im.cw + kTileW - 1) / kTileW) * ((im.ch + kTileH - 1) / kTileH);
     TraceArgs<R> a{sc, im, c};
     const bool count = c.segs || c.draws;
+    if (RT_PIXEL_QUEUE) {
+        if (!c.queue) return hipErrorInvalidValue;
+        const hipError_t e = hipMemsetAsync(c.queue, 0, sizeof(unsigned long long), stream);
+        if (e != hipSuccess) return e;
+    }
     if (walk != ACC_BRUTE) {
         const int mode = bvh_walk_mode(walk == ACC_BVH4);
         if (mode == ACC_BVH) launch_acc<R, ACC_BVH>(a, tiles, 0, count, stream);

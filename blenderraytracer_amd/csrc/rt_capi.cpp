@@ -361,7 +361,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     if (sums_in) HIP_TRY(hipMemcpyAsync(sc->sum.p, sums_in, 3 * n * sizeof(double), hipMemcpyHostToDevice, sc->stream));
     else HIP_TRY(hipMemsetAsync(sc->sum.p, 0, 3 * n * sizeof(double), sc->stream));
     HIP_TRY(hipMemsetAsync(sc->total.p, 0, 10 * sizeof(unsigned long long), sc->stream));
-    Counters c{sc->sum.p, nullptr, nullptr, sc->total.p};
+    Counters c{sc->sum.p, nullptr, nullptr, sc->total.p, sc->total.p + 9};
     if (want_segs) {
         HIP_TRY(sc->segs.ensure(n));
         HIP_TRY(hipMemsetAsync(sc->segs.p, 0, n * sizeof(uint32_t), sc->stream));
@@ -471,7 +471,7 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
     HIP_TRY(sc->total.ensure(10));
     HIP_TRY(hipMemsetAsync(sc->total.p, 0, 10 * sizeof(unsigned long long), st));
     ImageParams im = image_params(s, cw, ch);
-    Counters c{d_sum, nullptr, nullptr, sc->total.p};
+    Counters c{d_sum, nullptr, nullptr, sc->total.p, sc->total.p + 9};
     HIP_TRY(hipEventRecord(sc->ev[0], st));
     HIP_TRY(trace(sc, s, im, c, st));
     HIP_TRY(hipEventRecord(sc->ev[1], st));

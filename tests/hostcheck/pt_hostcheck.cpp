@@ -55,6 +55,17 @@ static int render(const rt_scene_desc* d, const rt_settings* s, double* sum, uin
     int stack[64];
     const BvhStack stk{stack, 1};
     const LdsSpheres no_lds{nullptr};
+#if PTC_QUEUE
+    // the pixel-queue loop (RT_PIXEL_QUEUE kernels), one lane taking every pixel in queue order
+    if (im.max_depth <= 0) return 0;
+    uint32_t head = 0;
+    auto fetch = [&head]() { return head++; };
+    if (s->accel == RT_ACCEL_BVH) trace_pixels_queue<R, true, ACC_BVH4>(v, im, fetch, sum, segs, draws, no_lds, stk);
+    else if (s->accel == 3) trace_pixels_queue<R, true, ACC_BVH>(v, im, fetch, sum, segs, draws, no_lds, stk);
+    else if (s->accel == 4) trace_pixels_queue<R, true, ACC_BVH_STACK>(v, im, fetch, sum, segs, draws, no_lds, stk);
+    else trace_pixels_queue<R, true, ACC_BRUTE>(v, im, fetch, sum, segs, draws, no_lds, stk);
+    return 0;
+#endif
     for (int cy = 0; cy < im.ch; ++cy)
         for (int cx = 0; cx < im.cw; ++cx) {
             const size_t q = (size_t)cy * im.cw + cx;

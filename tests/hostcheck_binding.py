@@ -61,14 +61,15 @@ def bvh_check(packed, n, seed):
     return bad, hits.value
 
 
-def render(packed, settings):
-    """Per-pixel linear means, segment and draw counts computed by the kernel's own code on the CPU."""
+def render(packed, settings, L=None):
+    """Per-pixel linear means, segment and draw counts computed by the kernel's own code on the CPU
+    (`L`: a variant library from lib(defines))."""
     cw = settings.crop_w or settings.width
     ch = settings.crop_h or settings.height
     s = np.zeros((ch, cw, 3))
     segs = np.zeros((ch, cw), dtype=np.uint32)
     draws = np.zeros((ch, cw), dtype=np.uint32)
-    rc = lib().ptc_render(C.byref(packed.desc), C.byref(settings), s.ctypes.data_as(C.POINTER(C.c_double)),
+    rc = (L or lib()).ptc_render(C.byref(packed.desc), C.byref(settings), s.ctypes.data_as(C.POINTER(C.c_double)),
                           segs.ctypes.data_as(C.POINTER(C.c_uint32)), draws.ctypes.data_as(C.POINTER(C.c_uint32)))
     assert rc == 0
     return {"mean": s / settings.samples, "segments": segs, "draws": draws}

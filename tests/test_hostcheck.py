@@ -58,6 +58,22 @@ def test_kernel_logic_bvh_matches_reference(case, walk):
     assert np.all(np.abs(r["mean"][ok] - lin[ok]) <= 1e-12 * np.maximum(1, np.abs(lin[ok])))
 
 
+@pytest.mark.parametrize("accel", [0, 4])
+@pytest.mark.parametrize("case", gc.case_names())
+def test_pixel_queue_loop_matches_reference(case, accel):
+    """trace_pixels_queue (the RT_PIXEL_QUEUE kernels' loop: a lane moves on to the next queued pixel
+    when its pixel is done) gives every pixel exactly trace_pixel's samples, segments and draws."""
+    rt, c = gc.tracer_for(case)
+    rt.accel = accel
+    r = hb.render(rt.packed(), rt.settings(crop=c["crop"]), hb.lib(("PTC_QUEUE=1",)))
+    assert np.array_equal(r["segments"], gc.load_array(case, "segs"))
+    assert np.array_equal(r["draws"], gc.load_array(case, "draws"))
+    lin = gc.load_array(case, "linear")
+    assert np.array_equal(np.isnan(r["mean"]), np.isnan(lin))
+    ok = ~np.isnan(lin)
+    assert np.all(np.abs(r["mean"][ok] - lin[ok]) <= 1e-12 * np.maximum(1, np.abs(lin[ok])))
+
+
 @pytest.mark.parametrize("scene,rays", [("rtow.json", 200_000), ("kitchen_sink.json", 200_000),
                                         ("sample_mesh.json", 200_000), ("cornell.json", 200_000), ("mesh50k", 4_000)])
 def test_bvh_closest_hit_identical_on_adversarial_rays(scene, rays):
