@@ -392,7 +392,7 @@ RT_HD bool bvh_node_hit(const BvhNode& n, const BvhRay& r, float tlimit) {
 
 struct Work {
     uint32_t nodes, spheres, tris;                // BVH nodes visited, sphere / triangle tests (stats)
-    uint32_t lane_trips, wave_trips;              // RT_PROFILE: walk iterations per lane / per wave
+    uint32_t lane_trips, wave_trips, uni_trips;   // RT_PROFILE: walk iterations per lane / per wave / uniform
 };
 #ifndef RT_BVH_COUNT
 #define RT_BVH_COUNT 1
@@ -428,6 +428,10 @@ RT_HD bool bvh_box_hit(const float* bx, const BvhRay& r, float tlimit, float& tn
 typedef float rt_f2 __attribute__((ext_vector_type(2)));
 #ifndef RT_BVH_WHILE_WHILE
 #define RT_BVH_WHILE_WHILE 0
+#endif
+
+#ifndef RT_BVH_UNIFORM
+#define RT_BVH_UNIFORM 1
 #endif
 
 // Both children of a two-child node: (lo - olo) * inv as fma(lo, inv, -olo * inv) for the pair of
@@ -493,23 +497,39 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
 #if RT_PROFILE && defined(__HIP_DEVICE_COMPILE__)
             ++w.lane_trips;                       // the first active lane counts the wave's iteration
             if ((int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) ++w.wave_trips;
+            {   // iterations in which every active lane is at the same inner node
+                const int first = __builtin_amdgcn_readfirstlane(cur);
+                const bool uni = __ballot(cur != first) == 0 && first >= 0;
+                if (uni && (int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) ++w.uni_trips;
+            }
 #endif
             if (cur >= 0) {
-                const Bvh2Node n = wide[cur];
                 RT_COUNT(++w.nodes);
-                float t0, t1;
-                bool h0, h1;
-                bvh_node2_hit(n, br, tl, h0, h1, t0, t1);
-                if (h0 && h1) {
-                    const bool swap = t1 < t0;
-                    stk.base[(sp++) * stk.stride] = swap ? n.child[0] : n.child[1];
-                    cur = swap ? n.child[1] : n.child[0];
-                    continue;
-                }
-                if (h0 | h1) {
-                    cur = h0 ? n.child[0] : n.child[1];
-                    continue;
-                }
+                auto step = [&](const Bvh2Node& n) -> bool {     // true: descend to the new cur
+                    float t0, t1;
+                    bool h0, h1;
+                    bvh_node2_hit(n, br, tl, h0, h1, t0, t1);
+                    if (h0 && h1) {
+                        const bool swap = t1 < t0;
+                        stk.base[(sp++) * stk.stride] = swap ? n.child[0] : n.child[1];
+                        cur = swap ? n.child[1] : n.child[0];
+                        return true;
+                    }
+                    if (h0 | h1) {
+                        cur = h0 ? n.child[0] : n.child[1];
+                        return true;
+                    }
+                    return false;
+                };
+#if RT_BVH_UNIFORM && defined(__HIP_DEVICE_COMPILE__)
+                // every active lane at the same node (30 % of RTOW walk steps, 49 % on mesh50k): read
+                // it with scalar loads, which bypass the vector memory pipeline
+                const int first = __builtin_amdgcn_readfirstlane(cur);
+                const bool down = __ballot(cur != first) == 0 ? step(wide[first]) : step(wide[cur]);
+#else
+                const bool down = step(wide[cur]);
+#endif
+                if (down) continue;
             } else {
                 leaf(~cur);
             }

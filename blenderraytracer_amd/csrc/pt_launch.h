@@ -7,6 +7,12 @@
 
 namespace rt {
 
+// Counters::totals slots: 0 segments, 1 BVH nodes, 2 sphere tests, 3 triangle tests; RT_PROFILE builds:
+// 4..6 cycles (closest hit, shading, regeneration), 7 / 8 walk iterations per lane / per wave, 9 wave
+// iterations whose active lanes all sit at one inner node; slot kQueueSlot: the pixel-queue head
+constexpr int kTotalSlots = 12;
+constexpr int kQueueSlot = 11;
+
 struct Counters {
     double* sum;               // n*3 running per-pixel radiance sums (read-modify-write)
     uint32_t* segs;            // optional n per-pixel world.hit counts

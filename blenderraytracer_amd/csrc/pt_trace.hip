@@ -120,8 +120,8 @@ void trace_kernel(const TraceArgs<R> args) {
                 for (int off = 32; off > 0; off >>= 1) v = max(v, (unsigned long long)__shfl_xor(v, off));
                 if (lane == 0) atomicAdd(args.c.totals + 4 + k, v);
             }
-            const uint32_t trips[2] = {r.work.lane_trips, r.work.wave_trips};
-            for (int k = 0; k < 2; ++k) {
+            const uint32_t trips[3] = {r.work.lane_trips, r.work.wave_trips, r.work.uni_trips};
+            for (int k = 0; k < 3; ++k) {
                 unsigned long long v = trips[k];
                 for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
                 if (lane == 0) atomicAdd(args.c.totals + 7 + k, v);

@@ -357,11 +357,11 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     const size_t n = (size_t)cw * ch;
     const bool want_segs = out && out->segments, want_draws = out && out->draws;
     HIP_TRY(sc->sum.ensure(3 * n));
-    HIP_TRY(sc->total.ensure(10));
+    HIP_TRY(sc->total.ensure(kTotalSlots));
     if (sums_in) HIP_TRY(hipMemcpyAsync(sc->sum.p, sums_in, 3 * n * sizeof(double), hipMemcpyHostToDevice, sc->stream));
     else HIP_TRY(hipMemsetAsync(sc->sum.p, 0, 3 * n * sizeof(double), sc->stream));
-    HIP_TRY(hipMemsetAsync(sc->total.p, 0, 10 * sizeof(unsigned long long), sc->stream));
-    Counters c{sc->sum.p, nullptr, nullptr, sc->total.p, sc->total.p + 9};
+    HIP_TRY(hipMemsetAsync(sc->total.p, 0, kTotalSlots * sizeof(unsigned long long), sc->stream));
+    Counters c{sc->sum.p, nullptr, nullptr, sc->total.p, sc->total.p + kQueueSlot};
     if (want_segs) {
         HIP_TRY(sc->segs.ensure(n));
         HIP_TRY(hipMemsetAsync(sc->segs.p, 0, n * sizeof(uint32_t), sc->stream));
@@ -409,7 +409,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     if (want_rgba) HIP_TRY(hipMemcpyAsync(out->rgba8, sc->rgba.p, 4 * n, hipMemcpyDeviceToHost, sc->stream));
     if (want_segs) HIP_TRY(hipMemcpyAsync(out->segments, sc->segs.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, sc->stream));
     if (want_draws) HIP_TRY(hipMemcpyAsync(out->draws, sc->draws.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, sc->stream));
-    unsigned long long totals[10] = {};
+    unsigned long long totals[kTotalSlots] = {};
     HIP_TRY(hipMemcpyAsync(totals, sc->total.p, sizeof totals, hipMemcpyDeviceToHost, sc->stream));
     HIP_TRY(hipStreamSynchronize(sc->stream));
     if (stats) {
@@ -423,9 +423,10 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
 #if RT_PROFILE
     const double cyc = (double)(totals[4] + totals[5] + totals[6]);
     fprintf(stderr, "[rt_profile] wave-max cycles: closest hit %.3f, shading %.3f, regeneration %.3f (%.3e total); "
-            "walk iterations: %.3e per lane, %.3e per wave, lane efficiency %.3f\n",
+            "walk iterations: %.3e per lane, %.3e per wave, lane efficiency %.3f, wave-uniform inner-node share %.3f\n",
             totals[4] / cyc, totals[5] / cyc, totals[6] / cyc, cyc, (double)totals[7], (double)totals[8],
-            totals[8] ? (double)totals[7] / (64.0 * (double)totals[8]) : 0.0);
+            totals[8] ? (double)totals[7] / (64.0 * (double)totals[8]) : 0.0,
+            totals[8] ? (double)totals[9] / (double)totals[8] : 0.0);
 #endif
     return RT_OK;
 }
@@ -468,15 +469,15 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
     if (rc) return rc;
     HIP_TRY(hipSetDevice(sc->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : sc->stream;
-    HIP_TRY(sc->total.ensure(10));
-    HIP_TRY(hipMemsetAsync(sc->total.p, 0, 10 * sizeof(unsigned long long), st));
+    HIP_TRY(sc->total.ensure(kTotalSlots));
+    HIP_TRY(hipMemsetAsync(sc->total.p, 0, kTotalSlots * sizeof(unsigned long long), st));
     ImageParams im = image_params(s, cw, ch);
-    Counters c{d_sum, nullptr, nullptr, sc->total.p, sc->total.p + 9};
+    Counters c{d_sum, nullptr, nullptr, sc->total.p, sc->total.p + kQueueSlot};
     HIP_TRY(hipEventRecord(sc->ev[0], st));
     HIP_TRY(trace(sc, s, im, c, st));
     HIP_TRY(hipEventRecord(sc->ev[1], st));
     if (sync || stats) {
-        unsigned long long totals[10] = {};
+        unsigned long long totals[kTotalSlots] = {};
         HIP_TRY(hipMemcpyAsync(totals, sc->total.p, sizeof totals, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         if (stats) {
