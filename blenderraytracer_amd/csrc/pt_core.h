@@ -531,7 +531,7 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
 #endif
                 if (down) continue;
             } else {
-                leaf(~cur);
+                leaf(~cur);      // (scalar leaf reads for wave-uniform leaves measured 2 % slower)
             }
             if (sp == 0) break;
             cur = stk.base[(--sp) * stk.stride];
