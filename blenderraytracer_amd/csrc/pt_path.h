@@ -175,10 +175,10 @@ RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int
 
 // Pixel-queue order: 8x8 blocks of the crop in raster order, the 64 pixels of a block consecutive, so
 // a wave's first fetch takes one whole block.  Positions past the crop's right/bottom edge are skipped.
-RT_HD inline uint32_t queue_length(const ImageParams& im) {
+RT_HD uint32_t queue_length(const ImageParams& im) {
     return (uint32_t)((im.cw + 7) / 8) * (uint32_t)((im.ch + 7) / 8) * 64u;
 }
-RT_HD inline bool queue_pixel(const ImageParams& im, uint32_t p, int& cx, int& cy) {
+RT_HD bool queue_pixel(const ImageParams& im, uint32_t p, int& cx, int& cy) {
     const uint32_t tiles_x = (uint32_t)(im.cw + 7) / 8, t = p >> 6, w = p & 63;
     cx = (int)((t % tiles_x) * 8 + (w & 7));
     cy = (int)((t / tiles_x) * 8 + (w >> 3));

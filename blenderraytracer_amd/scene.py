@@ -348,7 +348,7 @@ def scene_path(name):
 def load_scene_json(name):
     """Scene JSON by file name under scenes/ (mesh50k is generated on demand)."""
     p = scene_path(name)
-    if not os.path.exists(p) and os.path.basename(p) == "mesh50k.json":
+    if os.path.basename(p) == "mesh50k.json" and (not os.path.exists(p) or os.path.getsize(p) == 0):
         import importlib.util
         spec = importlib.util.spec_from_file_location("scenes_generate", os.path.join(SCENES_DIR, "generate.py"))
         gen = importlib.util.module_from_spec(spec)

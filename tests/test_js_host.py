@@ -29,10 +29,13 @@ MAT_DT = np.dtype([("type", "<i4"), ("_pad", "<i4"), ("albedo", "<f8", 3), ("rou
 
 def ensure_mesh50k():
     p = os.path.join(SCENES_DIR, "mesh50k.json")
-    if not os.path.exists(p):
-        from blenderraytracer_amd.scene import load_scene_json
-        with open(p, "w") as f:
-            json.dump(load_scene_json("mesh50k"), f)
+    if not os.path.exists(p) or os.path.getsize(p) == 0:
+        from blenderraytracer_amd import scene as sc
+        data = sc.load_scene_json("mesh50k")  # generated before the file exists (no empty-file race)
+        tmp = p + f".tmp{os.getpid()}"
+        with open(tmp, "w") as f:
+            json.dump(data, f)
+        os.replace(tmp, p)
 
 
 def run_tool(*args, env=None):
