@@ -75,12 +75,17 @@ template <class R> struct PlaneRec { R px, py, pz, nx, ny, nz; };
 template <class R> struct BoxRec { R mnx, mny, mnz, mxx, mxy, mxz; };
 template <class R> struct TriRec { R v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z, nx, ny, nz; };  // e1=v1-v0, e2=v2-v0
 template <class R> struct MatRec { int type, pad; R albedo[3]; R rough; R ior; R emit[3]; };
+// BVH leaf records in leaf order: everything one primitive test and its acceptance need (the
+// binary32 filter, the R-precision geometry, World index, World.objects index, material) in one
+// contiguous record, so a leaf issues all its loads at once instead of a chain of dependent ones.
+template <class R> struct SphereLeaf { SphereFilter f; SphereRec<R> s; int id, obj, mat, pad; };   // 64 B
+template <> struct SphereLeaf<float> { SphereRec<float> s; int id, obj, mat, pad; };                 // 32 B
+template <class R> struct TriLeaf { TriRec<R> t; int id, obj, mat, pad; };                            // 112 / 64 B
 
 // BVH node (32 B), nodes in depth-first preorder: an internal node's first child is the next node,
 // `skip` is the index just past its subtree.  fc = (first << 4) | count for a leaf of `count` <= 15
 // primitives at leaf-order positions [first, first+count), 0 for an internal node.
 struct BvhNode { float lo[3]; int skip; float hi[3]; int fc; };
-struct PrimKey { int id, obj; };   // index into the World-order arrays, World.objects index
 // The same tree as 64-B two-child nodes for the ordered stack walk: box k = {lo, hi} of child k,
 // child[k] >= 0 an inner node, < 0 the leaf ~fc.  Depth <= RT_BVH_STACK (scene_pack.h).
 // Bounds interleaved by child (lo[axis][child]) so both children's planes of an axis form one float2:
@@ -125,13 +130,10 @@ struct SceneView {
     const int* box_obj;
     const BvhNode* sphere_nodes;
     int num_sphere_nodes;
-    const SphereRec<R>* bvh_spheres;
-    const SphereFilter* bvh_sphere_filter;
-    const PrimKey* bvh_sphere_key;
+    const SphereLeaf<R>* bvh_sphere_leaf;
     const BvhNode* tri_nodes;
     int num_tri_nodes;
-    const TriRec<R>* bvh_tris;
-    const PrimKey* bvh_tri_key;
+    const TriLeaf<R>* bvh_tri_leaf;
     const Bvh2Node* sphere_wide;   // two-child nodes of the two trees (preorder)
     const Bvh2Node* tri_wide;
     int num_sphere_wide, num_tri_wide;
@@ -161,6 +163,21 @@ struct LdsSpheres { const SphereFilter* rec; };
 #define RT_PRAGMA(x) _Pragma(#x)
 #define RT_UNROLL(n) RT_PRAGMA(unroll n)
 
+#ifndef RT_SPHERE_AWAY
+#define RT_SPHERE_AWAY 0          // A/B option: measured -2 % on RTOW f64 (the branch saves nothing
+#endif                            // unless every lane of the wave takes it)
+// sphere_away_shortcut.  A ray whose origin is outside the sphere (c >= 0) and that moves away from
+// its centre (hb > 0) has both computed roots <= 0 < tMin, so the test can stop before sqrt and the
+// two divisions with the same answer: root1 = (-hb - sq)/a < 0, and with Y = RN(a c) >= 0,
+// disc = RN(RN(hb^2) - Y) <= RN(hb^2), so sq = RN(sqrt(disc)) <= RN(sqrt(RN(hb^2))) = hb (in binary
+// floating point, RN(sqrt(RN(h^2))) = h while h^2 neither overflows nor underflows: hence the range
+// check), and root2 = RN(RN(sq - hb)/a) <= 0.  tmin > 0 is required (World.hit's 0.001).
+template <class R>
+RT_HD bool sphere_moving_away(R hb, R c) {
+    return RT_SPHERE_AWAY && c >= (R)0 && hb > (R)(sizeof(R) == 8 ? 1e-150 : 1e-18) &&
+           hb < (R)(sizeof(R) == 8 ? 1e150 : 1e18);
+}
+
 // Sphere.hit (geometry.js:15-45) folded into World.hit's strict-< acceptance, in R arithmetic.
 template <class R>
 RT_HD void sphere_test_f64(const SceneView<R>& sc, V3<R> o, V3<R> d, R a, R tmin, int i, Closest<R>& b) {
@@ -168,6 +185,7 @@ RT_HD void sphere_test_f64(const SceneView<R>& sc, V3<R> o, V3<R> d, R a, R tmin
     R ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
     R hb = ocx * d.x + ocy * d.y + ocz * d.z;
     R c = (ocx * ocx + ocy * ocy + ocz * ocz) - s.r2;
+    if (sphere_moving_away(hb, c)) return;
     R disc = hb * hb - a * c;
     if (disc < (R)0) return;
     R sq = sqrt(disc);
@@ -319,6 +337,7 @@ RT_HD bool sphere_candidate(const SphereRec<R>& s, V3<R> o, V3<R> d, R a, R tmin
     R ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
     R hb = ocx * d.x + ocy * d.y + ocz * d.z;
     R c = (ocx * ocx + ocy * ocy + ocz * ocz) - s.r2;
+    if (sphere_moving_away(hb, c)) return false;
     R disc = hb * hb - a * c;
     if (disc < (R)0) return false;
     R sq = sqrt(disc);
@@ -393,7 +412,11 @@ RT_HD bool bvh_node_hit(const BvhNode& n, const BvhRay& r, float tlimit) {
 struct Work {
     uint32_t nodes, spheres, tris;                // BVH nodes visited, sphere / triangle tests (stats)
     uint32_t lane_trips, wave_trips, uni_trips;   // RT_PROFILE: walk iterations per lane / per wave / uniform
+    uint32_t x[4];                                // RT_WORK_EXTRA (host experiments): leaf-test breakdown
 };
+#ifndef RT_WORK_EXTRA
+#define RT_WORK_EXTRA 0
+#endif
 #ifndef RT_BVH_COUNT
 #define RT_BVH_COUNT 1
 #endif
@@ -426,6 +449,28 @@ RT_HD bool bvh_box_hit(const float* bx, const BvhRay& r, float tlimit, float& tn
 }
 
 typedef float rt_f2 __attribute__((ext_vector_type(2)));
+
+// RT_KEEP(x): make x live in a VGPR at this point of the program.  Used to pin a load that the
+// compiler would otherwise sink into a later branch (a dependent memory round trip) next to the
+// loads issued with it.  No-op on the host build.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RT_KEEP(x) asm("" : "+v"(x))   // not volatile: a volatile asm would count as a memory clobber
+                                        // and cost the walk its scalar node loads
+#else
+#define RT_KEEP(x) ((void)0)
+#endif
+#ifndef RT_NODE_PREFETCH
+#define RT_NODE_PREFETCH 1        // child indices loaded with the child boxes (one round trip per node)
+#endif
+#ifndef RT_LEAF_PREFETCH
+#define RT_LEAF_PREFETCH 0        // a leaf record's filter, geometry and keys loaded together
+#endif
+#ifndef RT_STACK_TOP
+#define RT_STACK_TOP 0            // the most recently pushed node kept in a register
+#endif
+#ifndef RT_WALK_IFIF
+#define RT_WALK_IFIF 0            // 1: one step (node, or leaf + pop) per loop iteration
+#endif
 #ifndef RT_BVH_WHILE_WHILE
 #define RT_BVH_WHILE_WHILE 0
 #endif
@@ -436,14 +481,22 @@ typedef float rt_f2 __attribute__((ext_vector_type(2)));
 
 // Both children of a two-child node: (lo - olo) * inv as fma(lo, inv, -olo * inv) for the pair of
 // children at once (same rounding as bvh_box_hit's FMA form).
+#ifndef RT_BVH_PACKED
+#define RT_BVH_PACKED 1           // 0: twelve scalar FMAs (no duplicated {inv, inv} register pairs)
+#endif
 RT_HD void bvh_node2_hit(const Bvh2Node& n, const BvhRay& r, float tlimit, bool& h0, bool& h1, float& t0,
                          float& t1) {
     rt_f2 a[3], b[3];
     for (int k = 0; k < 3; ++k) {
+#if RT_BVH_PACKED
         const rt_f2 inv = {r.inv[k], r.inv[k]};
         const rt_f2 slo = {-r.slo[k], -r.slo[k]}, shi = {-r.shi[k], -r.shi[k]};
         a[k] = __builtin_elementwise_fma(rt_f2{n.lo[k][0], n.lo[k][1]}, inv, slo);
         b[k] = __builtin_elementwise_fma(rt_f2{n.hi[k][0], n.hi[k][1]}, inv, shi);
+#else
+        a[k] = rt_f2{__builtin_fmaf(n.lo[k][0], r.inv[k], -r.slo[k]), __builtin_fmaf(n.lo[k][1], r.inv[k], -r.slo[k])};
+        b[k] = rt_f2{__builtin_fmaf(n.hi[k][0], r.inv[k], -r.shi[k]), __builtin_fmaf(n.hi[k][1], r.inv[k], -r.shi[k])};
+#endif
     }
     t0 = fmaxf(fmaxf(fminf(a[0].x, b[0].x), fminf(a[1].x, b[1].x)), fmaxf(fminf(a[2].x, b[2].x), 0.0f));
     t1 = fmaxf(fmaxf(fminf(a[0].y, b[0].y), fminf(a[1].y, b[1].y)), fmaxf(fminf(a[2].y, b[2].y), 0.0f));
@@ -493,6 +546,59 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
         }
 #else
         int sp = 0, cur = 0;
+#if RT_STACK_TOP
+        int top = RT_CHILD_EMPTY;   // never a node or leaf reference (leaves hold <= 15 primitives)
+#endif
+        auto push = [&](int c) {
+#if RT_STACK_TOP
+            if (top != RT_CHILD_EMPTY) stk.base[(sp++) * stk.stride] = top;
+            top = c;
+#else
+            stk.base[(sp++) * stk.stride] = c;
+#endif
+        };
+        auto pop = [&]() -> bool {    // false: the walk is over
+#if RT_STACK_TOP
+            if (top != RT_CHILD_EMPTY) {
+                cur = top;
+                top = RT_CHILD_EMPTY;
+                return true;
+            }
+#endif
+            if (sp == 0) return false;
+            cur = stk.base[(--sp) * stk.stride];
+            return true;
+        };
+        // true: descend to the new cur
+        auto step = [&](const Bvh2Node& n) -> bool {
+            float t0, t1;
+            bool h0, h1;
+            bvh_node2_hit(n, br, tl, h0, h1, t0, t1);
+#if RT_NODE_PREFETCH
+            // branch-free child selection: the child indices are consumed by selects ahead of any
+            // branch, so their loads issue with the box loads (no dependent round trip after the
+            // slab test)
+            const int c0 = n.child[0], c1 = n.child[1];
+            const bool both = h0 && h1;
+            const bool take1 = both ? (t1 < t0) : h1;
+            const int near_c = take1 ? c1 : c0, far_c = take1 ? c0 : c1;
+            if (both) push(far_c);
+            cur = (h0 | h1) ? near_c : cur;
+            return h0 | h1;
+#else
+            if (h0 && h1) {
+                const bool swap = t1 < t0;
+                push(swap ? n.child[0] : n.child[1]);
+                cur = swap ? n.child[1] : n.child[0];
+                return true;
+            }
+            if (h0 | h1) {
+                cur = h0 ? n.child[0] : n.child[1];
+                return true;
+            }
+            return false;
+#endif
+        };
         for (;;) {
 #if RT_PROFILE && defined(__HIP_DEVICE_COMPILE__)
             ++w.lane_trips;                       // the first active lane counts the wave's iteration
@@ -503,38 +609,24 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
                 if (uni && (int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) ++w.uni_trips;
             }
 #endif
+            bool down = false;
             if (cur >= 0) {
                 RT_COUNT(++w.nodes);
-                auto step = [&](const Bvh2Node& n) -> bool {     // true: descend to the new cur
-                    float t0, t1;
-                    bool h0, h1;
-                    bvh_node2_hit(n, br, tl, h0, h1, t0, t1);
-                    if (h0 && h1) {
-                        const bool swap = t1 < t0;
-                        stk.base[(sp++) * stk.stride] = swap ? n.child[0] : n.child[1];
-                        cur = swap ? n.child[1] : n.child[0];
-                        return true;
-                    }
-                    if (h0 | h1) {
-                        cur = h0 ? n.child[0] : n.child[1];
-                        return true;
-                    }
-                    return false;
-                };
 #if RT_BVH_UNIFORM && defined(__HIP_DEVICE_COMPILE__)
                 // every active lane at the same node (30 % of RTOW walk steps, 49 % on mesh50k): read
                 // it with scalar loads, which bypass the vector memory pipeline
                 const int first = __builtin_amdgcn_readfirstlane(cur);
-                const bool down = __ballot(cur != first) == 0 ? step(wide[first]) : step(wide[cur]);
+                down = __ballot(cur != first) == 0 ? step(wide[first]) : step(wide[cur]);
 #else
-                const bool down = step(wide[cur]);
+                down = step(wide[cur]);
 #endif
+#if !RT_WALK_IFIF
                 if (down) continue;
+#endif
             } else {
                 leaf(~cur);      // (scalar leaf reads for wave-uniform leaves measured 2 % slower)
             }
-            if (sp == 0) break;
-            cur = stk.base[(--sp) * stk.stride];
+            if (!down && !pop()) break;
         }
 #endif
     } else {
@@ -593,13 +685,31 @@ RT_HD void sphere_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R a, co
     const int first = fc >> 4, end = first + (fc & 15);
     RT_COUNT(w.spheres += end - first);
     for (int k = first; k < end; ++k) {
+        SphereLeaf<R> L = sc.bvh_sphere_leaf[k];
+#if RT_LEAF_PREFETCH
+        RT_KEEP(L.s.cx); RT_KEEP(L.s.cy); RT_KEEP(L.s.cz); RT_KEEP(L.s.r2);
+        RT_KEEP(L.id); RT_KEEP(L.obj); RT_KEEP(L.mat);
+#endif
         if constexpr (sizeof(R) == 8)
-            if (!sphere_filter_pass(sc.bvh_sphere_filter[k], fr)) continue;
+            if (!sphere_filter_pass(L.f, fr)) continue;
+#if RT_WORK_EXTRA
+        {   // x0: binary64 tests, x1: of those moving away from an outside centre (hb > 0, c >= 0),
+            // x2: candidates (t >= tmin), x3: accepted as the new best
+            ++w.x[0];
+            const R ocx = o.x - L.s.cx, ocy = o.y - L.s.cy, ocz = o.z - L.s.cz;
+            const R hb = ocx * d.x + ocy * d.y + ocz * d.z;
+            const R c = (ocx * ocx + ocy * ocy + ocz * ocz) - L.s.r2;
+            if (hb > (R)0 && c >= (R)0) ++w.x[1];
+        }
+#endif
         R t;
-        if (!sphere_candidate(sc.bvh_spheres[k], o, d, a, tmin, t)) continue;
-        const PrimKey key = sc.bvh_sphere_key[k];
-        if (better(t, key.obj, key.id, b)) {
-            b = Closest<R>{t, HIT_SPHERE, key.id, sc.sphere_mat[key.id], key.obj};
+        if (!sphere_candidate(L.s, o, d, a, tmin, t)) continue;
+#if RT_WORK_EXTRA
+        ++w.x[2];
+        if (better(t, L.obj, L.id, b)) ++w.x[3];
+#endif
+        if (better(t, L.obj, L.id, b)) {
+            b = Closest<R>{t, HIT_SPHERE, L.id, L.mat, L.obj};
             tl = bvh_tlimit(b.t);
         }
     }
@@ -610,11 +720,15 @@ RT_HD void tri_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R tmin, Cl
     const int first = fc >> 4, end = first + (fc & 15);
     RT_COUNT(w.tris += end - first);
     for (int k = first; k < end; ++k) {
+        TriLeaf<R> L = sc.bvh_tri_leaf[k];
+#if RT_LEAF_PREFETCH
+        RT_KEEP(L.t.v0x); RT_KEEP(L.t.e1x); RT_KEEP(L.t.e2x); RT_KEEP(L.t.nz);
+        RT_KEEP(L.id); RT_KEEP(L.obj); RT_KEEP(L.mat);
+#endif
         R t;
-        if (!triangle_candidate(sc.bvh_tris[k], o, d, tmin, t)) continue;
-        const PrimKey key = sc.bvh_tri_key[k];
-        if (better(t, key.obj, key.id, b)) {
-            b = Closest<R>{t, HIT_TRI, key.id, sc.tri_mat[key.id], key.obj};
+        if (!triangle_candidate(L.t, o, d, tmin, t)) continue;
+        if (better(t, L.obj, L.id, b)) {
+            b = Closest<R>{t, HIT_TRI, L.id, L.mat, L.obj};
             tl = bvh_tlimit(b.t);
         }
     }

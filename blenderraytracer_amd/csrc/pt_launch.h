@@ -19,11 +19,18 @@ struct Counters {
     uint32_t* draws;           // optional n per-pixel RNG draws
     unsigned long long* totals;   // optional [segments, BVH nodes, sphere tests, triangle tests]
     unsigned long long* queue = nullptr;   // pixel-queue head (RT_PIXEL_QUEUE builds), zeroed per launch
+    void* pool = nullptr;      // sample-pool radiance buffer (trace_uses_pool()): per-sample radiance
+    size_t pool_bytes = 0;     // of up to pool_bytes / (n * 3 * sizeof(R)) samples per launch
 };
 
 template <class R>
 // walk: ACC_BRUTE (World order), ACC_BVH_STACK (two-child BVH walk) or ACC_BVH4 (four-child walk)
 hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, int walk, hipStream_t stream);
+
+// true: launch_trace runs the sample-pool kernel, which needs Counters::pool (at least one sample of
+// the crop: n * 3 * sizeof(R) bytes); RT_SAMPLE_POOL=0 in the environment selects the lane-per-pixel
+// kernel (A/B runs, tests)
+bool trace_uses_pool();
 
 struct FinalizeParams {
     int n;

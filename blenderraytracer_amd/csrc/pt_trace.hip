@@ -1,11 +1,14 @@
 // pt_trace.hip — the path-tracing megakernel and its epilogue for gfx950 (MI355X).
 //
-// One lane owns one pixel of the crop window and traces that pixel's samples [s_begin, s_end) in
-// order (trace_pixel, pt_path.h).  Each wave covers an 8x8 pixel block, so neighbouring rays share a
-// wave.  BVH mode: every lane walks its own path through the two-child BVH with a per-lane stack in
-// LDS; brute-force mode: primitive records are walked in World.objects order by every lane in
-// lockstep, so all record loads are wave-uniform scalar loads.  The per-pixel sums are read and
-// written once per launch.
+// Default (sample pool, trace_pool_kernel): a wave owns an 8x8 pixel tile and one chunk of samples;
+// the tile's (pixel, sample) items are dealt to its lanes as they finish, per-sample radiance goes to
+// an HBM buffer and accumulate_kernel adds it to the per-pixel sums in sample order.
+// Lane-per-pixel (trace_kernel, RT_SAMPLE_POOL=0): one lane owns one pixel of the crop window and
+// traces that pixel's samples [s_begin, s_end) in order (trace_pixel, pt_path.h).
+// Either way each wave covers an 8x8 pixel block, so neighbouring rays share a wave.  BVH mode:
+// every lane walks its own path through the two-child BVH with a per-lane stack in LDS; brute-force
+// mode: primitive records are walked in World.objects order by every lane in lockstep, so all record
+// loads are wave-uniform scalar loads.
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -51,6 +54,31 @@ constexpr int kTileH = RT_WG_WAVES == 4 ? 16 : 8;
 template <class R, int ACC>
 constexpr int waves_per_simd() {
     return ACC >= ACC_BVH ? (sizeof(R) == 8 ? RT_BVH_WAVES_PER_SIMD : RT_BVH_WAVES_F32) : RT_MIN_WAVES_PER_SIMD;
+}
+
+// Per-wave reduction of the lanes' work counters into Counters::totals (one 64-bit atomic each).
+template <int ACC>
+__device__ __forceinline__ void add_totals(const Counters& c, const PixelResult& r, const int lane) {
+    if (!c.totals) return;
+    const uint32_t parts[4] = {r.segments, r.work.nodes, r.work.spheres, r.work.tris};
+    for (int k = 0; k < (ACC >= ACC_BVH ? 4 : 1); ++k) {
+        unsigned long long v = parts[k];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) atomicAdd(c.totals + k, v);
+    }
+    if constexpr (RT_PROFILE != 0) {
+        for (int k = 0; k < 3; ++k) {
+            unsigned long long v = r.cyc[k];
+            for (int off = 32; off > 0; off >>= 1) v = max(v, (unsigned long long)__shfl_xor(v, off));
+            if (lane == 0) atomicAdd(c.totals + 4 + k, v);
+        }
+        const uint32_t trips[3] = {r.work.lane_trips, r.work.wave_trips, r.work.uni_trips};
+        for (int k = 0; k < 3; ++k) {
+            unsigned long long v = trips[k];
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if (lane == 0) atomicAdd(c.totals + 7 + k, v);
+        }
+    }
 }
 
 template <class R, bool COUNT, int ACC>
@@ -107,27 +135,165 @@ void trace_kernel(const TraceArgs<R> args) {
         }
     }
 #endif
-    if (args.c.totals) {
-        const uint32_t parts[4] = {r.segments, r.work.nodes, r.work.spheres, r.work.tris};
-        for (int k = 0; k < (ACC >= ACC_BVH ? 4 : 1); ++k) {
-            unsigned long long v = parts[k];
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-            if (lane == 0) atomicAdd(args.c.totals + k, v);
-        }
-        if constexpr (RT_PROFILE != 0) {
-            for (int k = 0; k < 3; ++k) {
-                unsigned long long v = r.cyc[k];
-                for (int off = 32; off > 0; off >>= 1) v = max(v, (unsigned long long)__shfl_xor(v, off));
-                if (lane == 0) atomicAdd(args.c.totals + 4 + k, v);
-            }
-            const uint32_t trips[3] = {r.work.lane_trips, r.work.wave_trips, r.work.uni_trips};
-            for (int k = 0; k < 3; ++k) {
-                unsigned long long v = trips[k];
-                for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-                if (lane == 0) atomicAdd(args.c.totals + 7 + k, v);
-            }
-        }
+    add_totals<ACC>(args.c, r, lane);
+}
+
+// ---- sample pool (the default trace kernel) ----
+// A workgroup is one wave = one 8x8 tile of the crop x one chunk of up to `chunk` samples.  The tile's
+// (pixel, sample) items are dealt to the lanes from a wave-uniform counter in sample-major order as
+// lanes finish their samples, so a lane whose pixel is cheap (sky) goes on with the samples of its
+// neighbours instead of idling until the wave's slowest pixel is done; the lanes still hold pixels of
+// one 8x8 block (primary-ray coherence as in trace_kernel).  Each sample's radiance goes to
+// rad[s - s_begin][q][0..2]; accumulate_kernel then adds them to the per-pixel sums in sample order:
+// the same binary64 additions in the same order as trace_pixel, so the sums are bit-identical to
+// trace_kernel's (tests/test_gpu_parity.py::test_sample_pool_bit_identical).
+template <class R, bool COUNT, int ACC>
+__global__ __launch_bounds__(64, (waves_per_simd<R, ACC>()))
+void trace_pool_kernel(const TraceArgs<R> args, R* __restrict__ rad, const int tiles, const int chunk, const int rev) {
+    const ImageParams& im = args.im;
+    const SceneView<R>& sc = args.sc;
+    BvhStack stk{nullptr, 0};
+    if constexpr (ACC >= ACC_BVH_STACK) {
+        __shared__ int bvh_stack[(ACC == ACC_BVH4 ? RT_BVH4_STACK : RT_BVH_STACK) * 64];
+        stk.base = bvh_stack + threadIdx.x;
+        stk.stride = 64;
     }
+    const LdsSpheres lds{nullptr};
+    const int lane = threadIdx.x;
+    const int ci = blockIdx.x / tiles, tile = rev ? tiles - 1 - (int)(blockIdx.x % tiles) : blockIdx.x % tiles;
+    const int tiles_x = (im.cw + 7) / 8;
+    const int tx0 = (tile % tiles_x) * 8, ty0 = (tile / tiles_x) * 8;
+    const int vw = min(8, im.cw - tx0), nv = vw * min(8, im.ch - ty0);   // valid pixels of the tile
+    const int sb = im.s_begin + ci * chunk, se = min(im.s_end, sb + chunk);
+    const uint32_t total = (uint32_t)nv * (uint32_t)max(0, se - sb);
+    const size_t npix = (size_t)im.cw * im.ch;
+    PixelResult res{0, 0, {0, 0, 0}, {0, 0, 0}};
+    // the lane's current item: pixel (i, j) with key pkey at crop index q, sample s
+    int i = 0, j = 0, s = 0, depth = 0;
+    uint32_t pkey = 0, isegs = 0;
+    size_t q = 0;
+    Rng<R> g;
+    V3<R> o, d, T;
+    auto begin_item = [&](const uint32_t k) {
+        uint32_t m, sr;
+        if (nv == 64) { m = k & 63; sr = k >> 6; }
+        else { sr = k / (uint32_t)nv; m = k - sr * (uint32_t)nv; }
+        const int px = tx0 + (int)(m % (uint32_t)vw), py = ty0 + (int)(m / (uint32_t)vw);
+        const int row = im.y0 + py;
+        i = im.x0 + px;
+        j = im.height - 1 - row;
+        pkey = pixel_key(im.seedm, (uint32_t)row * (uint32_t)im.width + (uint32_t)i);
+        q = (size_t)py * im.cw + px;
+        s = sb + (int)sr;
+        T = mk<R>(1, 1, 1);
+        depth = im.max_depth;
+        isegs = 0;
+        start_sample(sc, im, i, j, pkey, s, g, o, d);
+    };
+    uint32_t next = 64;                       // items [0, 64) are dealt to lanes 0..63 up front
+    bool live = (uint32_t)lane < total;
+    if (live) begin_item((uint32_t)lane);
+    while (live) {                            // lanes only ever leave this loop, so every live lane
+        const uint64_t t0 = RT_TICK();        // has seen every update of `next`
+        const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, lds, res.work, stk);
+        const uint64_t t1 = RT_TICK();
+        if (RT_PROFILE) res.cyc[0] += t1 - t0;
+        ++res.segments;
+        ++isegs;
+        V3<R> L;
+        const bool done = shade_segment(sc, c, o, d, T, depth, g, L);
+        const uint64_t t2 = RT_TICK();
+        if (RT_PROFILE) res.cyc[1] += t2 - t1;
+        if (done) {
+            R* p = rad + ((size_t)(s - im.s_begin) * npix + q) * 3;
+            p[0] = L.x; p[1] = L.y; p[2] = L.z;
+            if (COUNT) {
+                if (args.c.segs) atomicAdd(args.c.segs + q, isegs);
+                if (args.c.draws) atomicAdd(args.c.draws + q, g.k);
+            }
+        }
+        const uint64_t need = __ballot(done);
+        if (done) {
+            const uint32_t k = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0));
+            live = k < total;
+            if (live) begin_item(k);
+        }
+        next += (uint32_t)__popcll(need);
+        if (RT_PROFILE) res.cyc[2] += RT_TICK() - t2;
+    }
+    add_totals<ACC>(args.c, res, lane);
+}
+
+// sum[q] += rad[s][q] for s = 0 .. ns-1 in order (binary64, as trace_pixel adds its samples)
+template <class R>
+__global__ __launch_bounds__(256) void accumulate_kernel(double* __restrict__ sum, const R* __restrict__ rad,
+                                                         const size_t npix, const int ns) {
+    const size_t q = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= npix) return;
+    double a0 = sum[3 * q], a1 = sum[3 * q + 1], a2 = sum[3 * q + 2];
+    const R* p = rad + 3 * q;
+    RT_UNROLL(8)
+    for (int s = 0; s < ns; ++s, p += 3 * npix) {
+        a0 += (double)p[0];
+        a1 += (double)p[1];
+        a2 += (double)p[2];
+    }
+    sum[3 * q] = a0; sum[3 * q + 1] = a1; sum[3 * q + 2] = a2;
+}
+
+bool trace_uses_pool() {
+    static int v = -1;
+    if (v == -1) {
+        const char* e = getenv("RT_SAMPLE_POOL");
+        v = !(e && e[0] == '0') && !RT_PIXEL_QUEUE;
+    }
+    return v == 1;
+}
+
+// tile order within a chunk (RT_POOL_ORDER=rev: last tile first; A/B runs)
+static int pool_rev() {
+    static int v = -1;
+    if (v == -1) {
+        const char* e = getenv("RT_POOL_ORDER");
+        v = e && e[0] == 'r';
+    }
+    return v;
+}
+
+// samples per pool wave (RT_POOL_CHUNK overrides: A/B runs)
+static int pool_chunk() {
+    static int v = 0;
+    if (!v) {
+        const char* e = getenv("RT_POOL_CHUNK");
+        v = e ? std::max(1, atoi(e)) : 24;   // measured 8/16/24/32/64: DESIGN.md
+    }
+    return v;
+}
+
+template <class R, int ACC>
+static hipError_t launch_pool(const TraceArgs<R>& a0, bool count, hipStream_t stream) {
+    const ImageParams& im = a0.im;
+    const size_t npix = (size_t)im.cw * im.ch, per_sample = npix * 3 * sizeof(R);
+    const size_t fit = a0.c.pool ? a0.c.pool_bytes / per_sample : 0;
+    if (fit < 1) return hipErrorInvalidValue;
+    const int ns_max = (int)std::min<size_t>(fit, (size_t)(im.s_end - im.s_begin));
+    const int tiles = ((im.cw + 7) / 8) * ((im.ch + 7) / 8), chunk = pool_chunk();
+    R* rad = static_cast<R*>(a0.c.pool);
+    for (int b = im.s_begin; b < im.s_end; b += ns_max) {
+        TraceArgs<R> a = a0;
+        a.im.s_begin = b;
+        a.im.s_end = std::min(im.s_end, b + ns_max);
+        const int ns = a.im.s_end - b, chunks = (ns + chunk - 1) / chunk;
+        if ((long long)tiles * chunks > 0x7FFFFFFFLL) return hipErrorInvalidConfiguration;
+        if (count) hipLaunchKernelGGL((trace_pool_kernel<R, true, ACC>), dim3(tiles * chunks), dim3(64), 0, stream, a, rad, tiles, chunk, pool_rev());
+        else hipLaunchKernelGGL((trace_pool_kernel<R, false, ACC>), dim3(tiles * chunks), dim3(64), 0, stream, a, rad, tiles, chunk, pool_rev());
+        hipLaunchKernelGGL(accumulate_kernel<R>, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream, a.c.sum,
+                           (const R*)rad, npix, ns);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 // RT_SPHERE_PATH=lds stages the 16-B sphere filter records in LDS per workgroup instead of reading them
@@ -165,7 +331,8 @@ static int device_cus() {
 }
 
 template <class R, int ACC>
-static void launch_acc(const TraceArgs<R>& a, int tiles, size_t lds_bytes, bool count, hipStream_t stream) {
+static hipError_t launch_acc(const TraceArgs<R>& a, int tiles, size_t lds_bytes, bool count, hipStream_t stream) {
+    if (ACC != ACC_LDS && trace_uses_pool()) return launch_pool<R, ACC>(a, count, stream);
     if (RT_PIXEL_QUEUE) {
         // one workgroup per resident wave slot (4 SIMDs per CU), never more than the queue's blocks
         const int slots = device_cus() * 4 * waves_per_simd<R, ACC>() / RT_WG_WAVES;
@@ -173,6 +340,7 @@ static void launch_acc(const TraceArgs<R>& a, int tiles, size_t lds_bytes, bool 
     }
     if (count) hipLaunchKernelGGL((trace_kernel<R, true, ACC>), dim3(tiles), dim3(kWgThreads), lds_bytes, stream, a);
     else hipLaunchKernelGGL((trace_kernel<R, false, ACC>), dim3(tiles), dim3(kWgThreads), lds_bytes, stream, a);
+    return hipGetLastError();
 }
 
 template <class R>
@@ -189,21 +357,16 @@ hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Cou
     }
     if (walk != ACC_BRUTE) {
         const int mode = bvh_walk_mode(walk == ACC_BVH4);
-        if (mode == ACC_BVH) launch_acc<R, ACC_BVH>(a, tiles, 0, count, stream);
-        else if (mode == ACC_BVH4) launch_acc<R, ACC_BVH4>(a, tiles, 0, count, stream);
-        else launch_acc<R, ACC_BVH_STACK>(a, tiles, 0, count, stream);
-        return hipGetLastError();
+        if (mode == ACC_BVH) return launch_acc<R, ACC_BVH>(a, tiles, 0, count, stream);
+        if (mode == ACC_BVH4) return launch_acc<R, ACC_BVH4>(a, tiles, 0, count, stream);
+        return launch_acc<R, ACC_BVH_STACK>(a, tiles, 0, count, stream);
     }
     const size_t lds_bytes = (size_t)sc.num_spheres * sizeof(SphereFilter);
     const bool lds = sizeof(R) == 8 && sc.num_spheres > 0 && lds_bytes <= 48 * 1024 && sphere_path_override() == 1;
     if constexpr (sizeof(R) == 8) {
-        if (lds) {
-            launch_acc<R, ACC_LDS>(a, tiles, lds_bytes, count, stream);
-            return hipGetLastError();
-        }
+        if (lds) return launch_acc<R, ACC_LDS>(a, tiles, lds_bytes, count, stream);
     }
-    launch_acc<R, ACC_BRUTE>(a, tiles, 0, count, stream);
-    return hipGetLastError();
+    return launch_acc<R, ACC_BRUTE>(a, tiles, 0, count, stream);
 }
 
 template hipError_t launch_trace<double>(const SceneView<double>&, const ImageParams&, const Counters&, int, hipStream_t);

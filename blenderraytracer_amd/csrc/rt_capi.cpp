@@ -96,18 +96,16 @@ struct DeviceScene {
     DevBuf<MatRec<R>> mats;
     DevBuf<int> plane_obj, box_obj;
     DevBuf<BvhNode> sphere_nodes, tri_nodes;
-    DevBuf<SphereRec<R>> bvh_spheres;
-    DevBuf<SphereFilter> bvh_sphere_filter;
-    DevBuf<PrimKey> bvh_sphere_key, bvh_tri_key;
-    DevBuf<TriRec<R>> bvh_tris;
+    DevBuf<SphereLeaf<R>> bvh_sphere_leaf;
+    DevBuf<TriLeaf<R>> bvh_tri_leaf;
     DevBuf<Bvh2Node> sphere_wide, tri_wide;
     DevBuf<Bvh4Node> sphere_wide4, tri_wide4;
     SceneView<R> view{};
     void release() {
         runs.release(); spheres.release(); sphere_filter.release(); sphere_r.release(); planes.release(); boxes.release(); tris.release();
         sphere_mat.release(); plane_mat.release(); box_mat.release(); tri_mat.release(); perm.release(); mats.release();
-        plane_obj.release(); box_obj.release(); sphere_nodes.release(); tri_nodes.release(); bvh_spheres.release();
-        bvh_sphere_filter.release(); bvh_sphere_key.release(); bvh_tri_key.release(); bvh_tris.release();
+        plane_obj.release(); box_obj.release(); sphere_nodes.release(); tri_nodes.release(); bvh_sphere_leaf.release();
+        bvh_tri_leaf.release();
         sphere_wide.release(); tri_wide.release(); sphere_wide4.release(); tri_wide4.release();
     }
 };
@@ -122,8 +120,7 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     UP(boxes, rec.boxes); UP(tris, rec.tris); UP(sphere_mat, hs.sphere_mat); UP(plane_mat, hs.plane_mat);
     UP(box_mat, hs.box_mat); UP(tri_mat, hs.tri_mat); UP(perm, rec.perm); UP(mats, rec.mats);
     UP(plane_obj, hs.plane_obj); UP(box_obj, hs.box_obj); UP(sphere_nodes, hs.sphere_bvh); UP(tri_nodes, hs.tri_bvh);
-    UP(bvh_spheres, rec.bvh_spheres); UP(bvh_sphere_filter, rec.bvh_sphere_filter); UP(bvh_sphere_key, rec.bvh_sphere_key);
-    UP(bvh_tri_key, rec.bvh_tri_key); UP(bvh_tris, rec.bvh_tris); UP(sphere_wide, hs.sphere_wide); UP(tri_wide, hs.tri_wide);
+    UP(bvh_sphere_leaf, rec.bvh_sphere_leaf); UP(bvh_tri_leaf, rec.bvh_tri_leaf); UP(sphere_wide, hs.sphere_wide); UP(tri_wide, hs.tri_wide);
     UP(sphere_wide4, hs.sphere_wide4); UP(tri_wide4, hs.tri_wide4);
 #undef UP
     if (e != hipSuccess) return fail(RT_ERR_DEVICE, "scene upload: %s", hipGetErrorString(e));
@@ -133,8 +130,7 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     v.tris = ds.tris.p; v.sphere_mat = ds.sphere_mat.p; v.plane_mat = ds.plane_mat.p; v.box_mat = ds.box_mat.p;
     v.tri_mat = ds.tri_mat.p; v.mats = ds.mats.p; v.perm = ds.perm.p;
     v.plane_obj = ds.plane_obj.p; v.box_obj = ds.box_obj.p; v.sphere_nodes = ds.sphere_nodes.p; v.tri_nodes = ds.tri_nodes.p;
-    v.bvh_spheres = ds.bvh_spheres.p; v.bvh_sphere_filter = ds.bvh_sphere_filter.p; v.bvh_sphere_key = ds.bvh_sphere_key.p;
-    v.bvh_tris = ds.bvh_tris.p; v.bvh_tri_key = ds.bvh_tri_key.p;
+    v.bvh_sphere_leaf = ds.bvh_sphere_leaf.p; v.bvh_tri_leaf = ds.bvh_tri_leaf.p;
     v.sphere_wide = ds.sphere_wide.p; v.tri_wide = ds.tri_wide.p;
     v.sphere_wide4 = ds.sphere_wide4.p; v.tri_wide4 = ds.tri_wide4.p;
     fill_view_constants(v, hs, d);
@@ -164,6 +160,7 @@ struct rt_scene {
     DevBuf<uint8_t> rgba;
     DevBuf<uint32_t> segs, draws;
     DevBuf<unsigned long long> total;
+    DevBuf<unsigned char> pool;     // sample-pool per-sample radiance (ensure_pool)
     std::atomic<int> cancel{0};
     size_t ckpt_pixels = 0;         // progressive state of the last rt_render / rt_render_resume:
     int ckpt_done = 0;              // `sum` holds samples [sample_begin, ckpt_done) of ckpt_pixels pixels
@@ -234,6 +231,35 @@ hipError_t trace(rt_scene* sc, const rt_settings* s, const ImageParams& im, cons
     const int walk = !use_bvh(sc, s) ? ACC_BRUTE : (sc->bvh4_ok ? ACC_BVH4 : ACC_BVH_STACK);
     if (s->precision == RT_PREC_F32) return launch_trace<float>(sc->s32.view, im, c, walk, st);
     return launch_trace<double>(sc->s64.view, im, c, walk, st);
+}
+
+// Sample-pool radiance buffer (trace_uses_pool, pt_trace.hip): every sample of the call when they fit
+// the budget (RT_POOL_MB, default 32 GiB of the 288 GB HBM, at most 40 % of the free device memory),
+// else as many whole samples as fit (launch_trace then splits the samples over several launches).
+// Kept by the scene between renders.
+int ensure_pool(rt_scene* sc, const rt_settings* s, size_t n, int samples, Counters& c) {
+    if (!trace_uses_pool() || samples <= 0 || n == 0) return RT_OK;
+    const size_t per_sample = n * 3 * (s->precision == RT_PREC_F32 ? sizeof(float) : sizeof(double));
+    static size_t budget = 0;
+    if (!budget) {
+        const char* e = getenv("RT_POOL_MB");
+        budget = (size_t)(e ? std::max(1LL, atoll(e)) : 32768LL) << 20;
+    }
+    size_t want = per_sample * (size_t)samples;
+    if (want > sc->pool.n) {
+        size_t free_b = 0, total_b = 0, cap = budget;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = std::min(cap, (free_b + sc->pool.n) / 10 * 4);
+        want = std::min(want, std::max<size_t>(cap / per_sample, 1) * per_sample);
+        while (want > sc->pool.n) {
+            if (sc->pool.ensure(want) == hipSuccess) break;
+            (void)hipGetLastError();
+            if (want == per_sample) return fail(RT_ERR_DEVICE, "sample pool: cannot allocate %zu bytes", per_sample);
+            want = std::max<size_t>(want / per_sample / 2, 1) * per_sample;
+        }
+    }
+    c.pool = sc->pool.p;
+    c.pool_bytes = sc->pool.n;
+    return RT_OK;
 }
 
 // totals = [segments, BVH nodes, sphere tests, triangle tests] of the launches
@@ -326,7 +352,7 @@ void rt_scene_destroy(rt_scene* sc) {
     sc->s64.release();
     sc->s32.release();
     sc->sum.release(); sc->mean.release(); sc->post.release(); sc->post_raw.release(); sc->rgba.release();
-    sc->segs.release(); sc->draws.release(); sc->total.release();
+    sc->segs.release(); sc->draws.release(); sc->total.release(); sc->pool.release();
     for (auto& e : sc->ev)
         if (e) (void)hipEventDestroy(e);
     if (sc->stream) (void)hipStreamDestroy(sc->stream);
@@ -376,6 +402,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     im.s_begin = std::max(im.s_begin, first);
     const int s0 = im.s_begin, s1 = std::max(im.s_end, s0);
     const int batch = s->batch_samples > 0 ? s->batch_samples : std::max(1, s1 - s0);
+    if (s->max_depth > 0 && (rc = ensure_pool(sc, s, n, std::min(batch, s1 - s0), c))) return rc;
     sc->ckpt_pixels = n;
     sc->ckpt_done = s0;
     double kernel_ms = 0;
@@ -473,6 +500,7 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
     HIP_TRY(hipMemsetAsync(sc->total.p, 0, kTotalSlots * sizeof(unsigned long long), st));
     ImageParams im = image_params(s, cw, ch);
     Counters c{d_sum, nullptr, nullptr, sc->total.p, sc->total.p + kQueueSlot};
+    if (s->max_depth > 0 && (rc = ensure_pool(sc, s, (size_t)cw * ch, im.s_end - im.s_begin, c))) return rc;
     HIP_TRY(hipEventRecord(sc->ev[0], st));
     HIP_TRY(trace(sc, s, im, c, st));
     HIP_TRY(hipEventRecord(sc->ev[1], st));

@@ -150,6 +150,9 @@ struct BvhBuilder {
 #ifndef RT_BVH_BINS
 #define RT_BVH_BINS 16
 #endif
+#ifndef RT_BVH_SWEEP
+#define RT_BVH_SWEEP 0            // 1: full-sweep SAH over all three axes instead of binned on the widest
+#endif
     static constexpr int kLeafMax = RT_BVH_LEAF;   // primitives per leaf (<= 15)
     static constexpr int kBins = RT_BVH_BINS;      // SAH bins
 
@@ -194,7 +197,38 @@ struct BvhBuilder {
         const double extent = chi[axis] - clo[axis];
         int mid = -1;
         const bool force_median = depth + 1 + median_levels(count) >= RT_BVH_STACK;
-        if (count > kLeafMax && extent > 0 && !force_median) {
+        if (RT_BVH_SWEEP && count > kLeafMax && extent > 0 && !force_median) {
+            // full-sweep SAH: every object split along every axis (centroid order)
+            double best = INFINITY;
+            int best_axis = -1, best_i = -1;
+            std::vector<double> right_area(count + 1);
+            for (int a = 0; a < 3; ++a) {
+                if (!(chi[a] - clo[a] > 0)) continue;
+                std::sort(prims.begin() + begin, prims.begin() + end,
+                          [&](const BuildPrim& p, const BuildPrim& q) { return p.c[a] < q.c[a] || (p.c[a] == q.c[a] && p.idx < q.idx); });
+                double blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                for (int i = count - 1; i >= 1; --i) {
+                    const BuildPrim& p = prims[begin + i];
+                    for (int k = 0; k < 3; ++k) { blo[k] = std::min(blo[k], p.lo[k]); bhi[k] = std::max(bhi[k], p.hi[k]); }
+                    right_area[i] = area(blo, bhi);
+                }
+                for (int k = 0; k < 3; ++k) { blo[k] = INFINITY; bhi[k] = -INFINITY; }
+                for (int i = 1; i < count; ++i) {
+                    const BuildPrim& p = prims[begin + i - 1];
+                    for (int k = 0; k < 3; ++k) { blo[k] = std::min(blo[k], p.lo[k]); bhi[k] = std::max(bhi[k], p.hi[k]); }
+                    const double cost = i * area(blo, bhi) + (count - i) * right_area[i];
+                    if (cost < best) { best = cost; best_axis = a; best_i = i; }
+                }
+            }
+            if (best_axis >= 0) {
+                std::sort(prims.begin() + begin, prims.begin() + end, [&](const BuildPrim& p, const BuildPrim& q) {
+                    return p.c[best_axis] < q.c[best_axis] || (p.c[best_axis] == q.c[best_axis] && p.idx < q.idx);
+                });
+                mid = begin + best_i;
+            } else {
+                mid = (begin + end) / 2;
+            }
+        } else if (count > kLeafMax && extent > 0 && !force_median) {
             // binned SAH along the widest centroid axis
             struct Bin { double lo[3], hi[3]; int n; };
             Bin bins[kBins];
@@ -403,11 +437,10 @@ struct HostRecords {
     std::vector<TriRec<R>> tris;
     std::vector<MatRec<R>> mats;
     std::vector<int> perm;
-    // BVH leaf order copies (bvh_spheres[k] = spheres[bvh_sphere_key[k].id], same for triangles)
-    std::vector<SphereRec<R>> bvh_spheres;
-    std::vector<SphereFilter> bvh_sphere_filter;
-    std::vector<PrimKey> bvh_sphere_key, bvh_tri_key;
-    std::vector<TriRec<R>> bvh_tris;
+    // BVH leaf-order records (bvh_sphere_leaf[k] describes spheres[bvh_sphere_leaf[k].id], same for
+    // triangles)
+    std::vector<SphereLeaf<R>> bvh_sphere_leaf;
+    std::vector<TriLeaf<R>> bvh_tri_leaf;
 };
 
 template <class R>
@@ -458,14 +491,16 @@ void make_records(const HostScene& hs, const rt_scene_desc& d, HostRecords<R>& o
     }
     out.perm.assign(d.perm, d.perm + 512);
     for (int id : hs.sphere_bvh_prims) {
-        out.bvh_spheres.push_back(out.spheres[id]);
-        out.bvh_sphere_filter.push_back(out.sphere_filter[id]);
-        out.bvh_sphere_key.push_back(PrimKey{id, hs.sphere_obj[id]});
+        SphereLeaf<R> L{};
+        if constexpr (sizeof(R) == 8) L.f = out.sphere_filter[id];
+        L.s = out.spheres[id];
+        L.id = id;
+        L.obj = hs.sphere_obj[id];
+        L.mat = hs.sphere_mat[id];
+        out.bvh_sphere_leaf.push_back(L);
     }
-    for (int id : hs.tri_bvh_prims) {
-        out.bvh_tris.push_back(out.tris[id]);
-        out.bvh_tri_key.push_back(PrimKey{id, hs.tri_obj[id]});
-    }
+    for (int id : hs.tri_bvh_prims)
+        out.bvh_tri_leaf.push_back(TriLeaf<R>{out.tris[id], id, hs.tri_obj[id], hs.tri_mat[id], 0});
 }
 
 // Camera / background constants of the SceneView (pointers are set by the caller).

@@ -27,8 +27,7 @@ struct HostView {
         v.mats = rec.mats.data(); v.perm = rec.perm.data();
         v.plane_obj = hs.plane_obj.data(); v.box_obj = hs.box_obj.data();
         v.sphere_nodes = hs.sphere_bvh.data(); v.tri_nodes = hs.tri_bvh.data();
-        v.bvh_spheres = rec.bvh_spheres.data(); v.bvh_sphere_filter = rec.bvh_sphere_filter.data();
-        v.bvh_sphere_key = rec.bvh_sphere_key.data(); v.bvh_tris = rec.bvh_tris.data(); v.bvh_tri_key = rec.bvh_tri_key.data();
+        v.bvh_sphere_leaf = rec.bvh_sphere_leaf.data(); v.bvh_tri_leaf = rec.bvh_tri_leaf.data();
         v.sphere_wide = hs.sphere_wide.data(); v.tri_wide = hs.tri_wide.data();
         v.sphere_wide4 = hs.sphere_wide4.data(); v.tri_wide4 = hs.tri_wide4.data();
         fill_view_constants(v, hs, *d);
@@ -219,5 +218,34 @@ extern "C" int ptc_bvh_info(const rt_scene_desc* d, int* depth, int* stack4, int
     *stack4 = hv.hs.bvh4_stack;
     *nodes2 = (int)(hv.hs.sphere_wide.size() + hv.hs.tri_wide.size());
     *nodes4 = (int)(hv.hs.sphere_wide4.size() + hv.hs.tri_wide4.size());
+    return 0;
+}
+
+// Work totals of the two-child walk over a crop (host experiments on BVH quality, TEST/DEV TOOL):
+// out = {segments, nodes, sphere tests, triangle tests, x0..x3 (RT_WORK_EXTRA)}
+extern "C" int ptc_work(const rt_scene_desc* d, const rt_settings* s, double* out) {
+    HostView<double> hv;
+    if (!hv.init(d)) return -1;
+    ImageParams im{};
+    im.width = s->width; im.height = s->height;
+    im.x0 = s->crop_x0; im.y0 = s->crop_y0;
+    im.cw = s->crop_w > 0 ? s->crop_w : s->width;
+    im.ch = s->crop_h > 0 ? s->crop_h : s->height;
+    im.samples = s->samples;
+    im.s_begin = 0;
+    im.s_end = s->samples;
+    im.max_depth = s->max_depth;
+    im.aa_mode = s->aa_mode;
+    im.seedm = host_seed_mix(s->seed);
+    int stack[64];
+    const BvhStack stk{stack, 1};
+    for (int k = 0; k < 8; ++k) out[k] = 0;
+    for (int cy = 0; cy < im.ch; ++cy)
+        for (int cx = 0; cx < im.cw; ++cx) {
+            double acc[3] = {0, 0, 0};
+            const PixelResult r = trace_pixel<double, true, ACC_BVH_STACK>(hv.v, im, cx, cy, im.s_end, acc, LdsSpheres{nullptr}, stk);
+            out[0] += r.segments; out[1] += r.work.nodes; out[2] += r.work.spheres; out[3] += r.work.tris;
+            for (int k = 0; k < 4; ++k) out[4 + k] += r.work.x[k];
+        }
     return 0;
 }

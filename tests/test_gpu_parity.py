@@ -235,21 +235,61 @@ np.savez(sys.argv[2], **out)
 '''
 
 
-@pytest.mark.parametrize("walk", ["four", "skip"])
-def test_alternative_bvh_walks_bit_identical(gpu, tmp_path, walk):
-    """The A/B walks (RT_BVH_WALK=four: four-child nodes; skip: stackless preorder) render the same
-    bits as the default two-child walk (run in child processes: the walk is chosen per process)."""
+def _render_in_child(script, path, **env):
+    """Run `script` in a child process (the trace-kernel choices are read once per process)."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    res = {}
-    for mode in ("two", walk):
-        f = tmp_path / f"{mode}.npz"
-        env = dict(os.environ, RT_BVH_WALK=mode)
-        r = subprocess.run([sys.executable, "-c", _WALK_SCRIPT, root, str(f)], env=env, capture_output=True,
-                           text=True, timeout=600)
-        assert r.returncode == 0, r.stderr[-2000:]
-        res[mode] = np.load(f)
+    r = subprocess.run([sys.executable, "-c", script, root, str(path)], env=dict(os.environ, **env),
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return np.load(path)
+
+
+@pytest.mark.parametrize("walk", ["four", "skip"])
+def test_alternative_bvh_walks_bit_identical(gpu, tmp_path, walk):
+    """The A/B walks (RT_BVH_WALK=four: four-child nodes; skip: stackless preorder) render the same
+    bits as the default two-child walk (run in child processes: the walk is chosen per process)."""
+    res = {mode: _render_in_child(_WALK_SCRIPT, tmp_path / f"{mode}.npz", RT_BVH_WALK=mode) for mode in ("two", walk)}
     for k in res["two"].files:
         assert np.array_equal(res["two"][k], res[walk][k], equal_nan=True), k
+
+
+_POOL_SCRIPT = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import torch  # noqa: F401  (HIP runtime first)
+from blenderraytracer_amd import capi
+from blenderraytracer_amd.renderer import GpuRayTracer
+from blenderraytracer_amd.scene import load_scene_json
+out = {}
+for name, w, h, crop, prec, accel, spp in (
+        ("mesh50k", 1920, 1080, (900, 480, 61, 43), capi.RT_PREC_F64, capi.RT_ACCEL_BVH, 5),
+        ("kitchen_sink.json", 96, 64, None, capi.RT_PREC_F64, capi.RT_ACCEL_BVH, 7),
+        ("kitchen_sink.json", 96, 64, None, capi.RT_PREC_F64, capi.RT_ACCEL_BRUTE, 7),
+        ("cornell.json", 52, 37, None, capi.RT_PREC_F64, capi.RT_ACCEL_AUTO, 9),
+        ("rtow.json", 163, 91, None, capi.RT_PREC_F64, capi.RT_ACCEL_BVH, 7),
+        ("rtow.json", 163, 91, None, capi.RT_PREC_F32, capi.RT_ACCEL_BVH, 7)):
+    rt = GpuRayTracer(w, h, seed=9, accel=accel, precision=prec)
+    assert rt.load_from_json(load_scene_json(name))
+    rt.update_render_settings({"samples": spp, "maxBounces": 5})
+    r = rt.render(crop=crop, want=("mean", "segments", "draws"))
+    for k in ("mean", "segments", "draws"):
+        out[f"{name}.{prec}.{accel}.{k}"] = r[k]
+    out[f"{name}.{prec}.{accel}.batched"] = rt.render(crop=crop, want=("mean",), batch_samples=3)["mean"]
+np.savez(sys.argv[2], **out)
+'''
+
+
+@pytest.mark.parametrize("env", [{"RT_SAMPLE_POOL": "0"}, {"RT_POOL_MB": "1", "RT_POOL_CHUNK": "2"}],
+                         ids=["lane_per_pixel", "split_launches"])
+def test_sample_pool_bit_identical(gpu, tmp_path, env):
+    """The sample-pool kernel (default: lanes take (pixel, sample) items of their 8x8 tile, radiance
+    added to the sums in sample order by accumulate_kernel) renders the same bits as the lane-per-pixel
+    kernel (RT_SAMPLE_POOL=0), also when a 1-MiB pool splits the samples over many launches and
+    waves hold 2-sample chunks; ragged tiles, both precisions, BVH and brute force, counters."""
+    base = _render_in_child(_POOL_SCRIPT, tmp_path / "pool.npz")
+    other = _render_in_child(_POOL_SCRIPT, tmp_path / "other.npz", **env)
+    for k in base.files:
+        assert np.array_equal(base[k], other[k], equal_nan=True), k
