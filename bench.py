@@ -92,7 +92,8 @@ def cpu_baseline(rt, cfg, side):
 
 
 def load_traffic(workload, precision):
-    """HBM bytes per trace launch from the rocprofv3 PMC passes (profiles/pmc_<workload>_<prec>.json)."""
+    """HBM bytes per trace step (trace_pool_kernel + accumulate_kernel) from the rocprofv3 PMC passes
+    (profiles/pmc_<workload>_<prec>.json, written by scripts/profile_round.sh)."""
     p = os.path.join(ROOT, "profiles", f"pmc_{workload}_{precision}.json")
     if os.path.exists(p):
         with open(p) as f:
@@ -183,7 +184,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": "trace_kernel", "kernel_ms": round(k_ms, 3),
+                         "kernel": "trace_pool_kernel + accumulate_kernel (one launch each per frame)",
+                         "kernel_ms": round(k_ms, 3),
                          "algorithmic_bytes_per_launch": a_bytes,
                          "definition": ("BVH: 64 B/node visited + 16 B/sphere + 36 B/triangle tested + segments x "
                                         "24 B/plane|box + 12 B/pixel" if bvh else

@@ -20,7 +20,7 @@ struct Counters {
     unsigned long long* totals;   // optional [segments, BVH nodes, sphere tests, triangle tests]
     unsigned long long* queue = nullptr;   // pixel-queue head (RT_PIXEL_QUEUE builds), zeroed per launch
     void* pool = nullptr;      // sample-pool radiance buffer (trace_uses_pool()): per-sample radiance
-    size_t pool_bytes = 0;     // of up to pool_bytes / (n * 3 * sizeof(R)) samples per launch
+    size_t pool_bytes = 0;     // of up to pool_bytes / pool_sample_bytes(cw, ch, sizeof(R)) samples per launch
 };
 
 template <class R>
@@ -28,9 +28,13 @@ template <class R>
 hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, int walk, hipStream_t stream);
 
 // true: launch_trace runs the sample-pool kernel, which needs Counters::pool (at least one sample of
-// the crop: n * 3 * sizeof(R) bytes); RT_SAMPLE_POOL=0 in the environment selects the lane-per-pixel
+// the crop: pool_sample_bytes); RT_SAMPLE_POOL=0 in the environment selects the lane-per-pixel
 // kernel (A/B runs, tests)
 bool trace_uses_pool();
+// bytes the pool holds per sample of a cw x ch crop: 64 pixels per 8x8 tile (edge tiles padded)
+inline size_t pool_sample_bytes(int cw, int ch, size_t real_bytes) {
+    return (size_t)((cw + 7) / 8) * (size_t)((ch + 7) / 8) * 64 * 3 * real_bytes;
+}
 
 struct FinalizeParams {
     int n;

@@ -144,7 +144,8 @@ void trace_kernel(const TraceArgs<R> args) {
 // lanes finish their samples, so a lane whose pixel is cheap (sky) goes on with the samples of its
 // neighbours instead of idling until the wave's slowest pixel is done; the lanes still hold pixels of
 // one 8x8 block (primary-ray coherence as in trace_kernel).  Each sample's radiance goes to
-// rad[s - s_begin][q][0..2]; accumulate_kernel then adds them to the per-pixel sums in sample order:
+// rad[tile][s - s_begin][m][0..2] (m = pixel of the tile: a wave writes one contiguous region, whole
+// cache lines); accumulate_kernel then adds them to the per-pixel sums in sample order:
 // the same binary64 additions in the same order as trace_pixel, so the sums are bit-identical to
 // trace_kernel's (tests/test_gpu_parity.py::test_sample_pool_bit_identical).
 template <class R, bool COUNT, int ACC>
@@ -166,16 +167,16 @@ void trace_pool_kernel(const TraceArgs<R> args, R* __restrict__ rad, const int t
     const int vw = min(8, im.cw - tx0), nv = vw * min(8, im.ch - ty0);   // valid pixels of the tile
     const int sb = im.s_begin + ci * chunk, se = min(im.s_end, sb + chunk);
     const uint32_t total = (uint32_t)nv * (uint32_t)max(0, se - sb);
-    const size_t npix = (size_t)im.cw * im.ch;
+    const int ns = im.s_end - im.s_begin;     // samples of this launch
     PixelResult res{0, 0, {0, 0, 0}, {0, 0, 0}};
-    // the lane's current item: pixel (i, j) with key pkey at crop index q, sample s
+    // the lane's current item: pixel m of the tile = (i, j) with key pkey at crop index q, sample s
     int i = 0, j = 0, s = 0, depth = 0;
-    uint32_t pkey = 0, isegs = 0;
+    uint32_t m = 0, pkey = 0, isegs = 0;
     size_t q = 0;
     Rng<R> g;
     V3<R> o, d, T;
     auto begin_item = [&](const uint32_t k) {
-        uint32_t m, sr;
+        uint32_t sr;
         if (nv == 64) { m = k & 63; sr = k >> 6; }
         else { sr = k / (uint32_t)nv; m = k - sr * (uint32_t)nv; }
         const int px = tx0 + (int)(m % (uint32_t)vw), py = ty0 + (int)(m / (uint32_t)vw);
@@ -205,7 +206,7 @@ void trace_pool_kernel(const TraceArgs<R> args, R* __restrict__ rad, const int t
         const uint64_t t2 = RT_TICK();
         if (RT_PROFILE) res.cyc[1] += t2 - t1;
         if (done) {
-            R* p = rad + ((size_t)(s - im.s_begin) * npix + q) * 3;
+            R* p = rad + (((size_t)tile * ns + (size_t)(s - im.s_begin)) * 64 + m) * 3;
             p[0] = L.x; p[1] = L.y; p[2] = L.z;
             if (COUNT) {
                 if (args.c.segs) atomicAdd(args.c.segs + q, isegs);
@@ -225,16 +226,22 @@ void trace_pool_kernel(const TraceArgs<R> args, R* __restrict__ rad, const int t
     add_totals<ACC>(args.c, res, lane);
 }
 
-// sum[q] += rad[s][q] for s = 0 .. ns-1 in order (binary64, as trace_pixel adds its samples)
+// sum[q] += rad[tile][s][m] for s = 0 .. ns-1 in order (binary64, as trace_pixel adds its samples);
+// one thread per pixel, a wave per tile (its reads of one sample are 64 x 3 contiguous values)
 template <class R>
-__global__ __launch_bounds__(256) void accumulate_kernel(double* __restrict__ sum, const R* __restrict__ rad,
-                                                         const size_t npix, const int ns) {
-    const size_t q = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (q >= npix) return;
+__global__ __launch_bounds__(256) void accumulate_kernel(const ImageParams im, double* __restrict__ sum,
+                                                         const R* __restrict__ rad, const int tiles, const int ns) {
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6), m = threadIdx.x & 63;
+    if (tile >= tiles) return;
+    const int tiles_x = (im.cw + 7) / 8;
+    const int tx0 = (tile % tiles_x) * 8, ty0 = (tile / tiles_x) * 8;
+    const int vw = min(8, im.cw - tx0), nv = vw * min(8, im.ch - ty0);
+    if (m >= nv) return;
+    const size_t q = (size_t)(ty0 + m / vw) * im.cw + (tx0 + m % vw);
     double a0 = sum[3 * q], a1 = sum[3 * q + 1], a2 = sum[3 * q + 2];
-    const R* p = rad + 3 * q;
+    const R* p = rad + ((size_t)tile * ns * 64 + m) * 3;
     RT_UNROLL(8)
-    for (int s = 0; s < ns; ++s, p += 3 * npix) {
+    for (int s = 0; s < ns; ++s, p += 64 * 3) {
         a0 += (double)p[0];
         a1 += (double)p[1];
         a2 += (double)p[2];
@@ -261,24 +268,26 @@ static int pool_rev() {
     return v;
 }
 
-// samples per pool wave (RT_POOL_CHUNK overrides: A/B runs)
-static int pool_chunk() {
-    static int v = 0;
-    if (!v) {
+// Samples per pool wave: about 20 chunks per tile (measured best on RTOW 512 spp, 24 samples, and on
+// mesh50k 256 spp, 12; Cornell 64 spp: 4, which fills the chip: a frame's last waves are then short,
+// while a wave still deals >= 4 items per lane); RT_POOL_CHUNK overrides (A/B runs)
+static int pool_chunk(int ns) {
+    static int v = -1;
+    if (v == -1) {
         const char* e = getenv("RT_POOL_CHUNK");
-        v = e ? std::max(1, atoi(e)) : 24;   // measured 8/16/24/32/64: DESIGN.md
+        v = e ? std::max(1, atoi(e)) : 0;
     }
-    return v;
+    return v ? v : std::min(64, std::max(4, (ns + 19) / 20));
 }
 
 template <class R, int ACC>
 static hipError_t launch_pool(const TraceArgs<R>& a0, bool count, hipStream_t stream) {
     const ImageParams& im = a0.im;
-    const size_t npix = (size_t)im.cw * im.ch, per_sample = npix * 3 * sizeof(R);
+    const size_t per_sample = pool_sample_bytes(im.cw, im.ch, sizeof(R));
     const size_t fit = a0.c.pool ? a0.c.pool_bytes / per_sample : 0;
     if (fit < 1) return hipErrorInvalidValue;
     const int ns_max = (int)std::min<size_t>(fit, (size_t)(im.s_end - im.s_begin));
-    const int tiles = ((im.cw + 7) / 8) * ((im.ch + 7) / 8), chunk = pool_chunk();
+    const int tiles = ((im.cw + 7) / 8) * ((im.ch + 7) / 8), chunk = pool_chunk(ns_max);
     R* rad = static_cast<R*>(a0.c.pool);
     for (int b = im.s_begin; b < im.s_end; b += ns_max) {
         TraceArgs<R> a = a0;
@@ -288,8 +297,8 @@ static hipError_t launch_pool(const TraceArgs<R>& a0, bool count, hipStream_t st
         if ((long long)tiles * chunks > 0x7FFFFFFFLL) return hipErrorInvalidConfiguration;
         if (count) hipLaunchKernelGGL((trace_pool_kernel<R, true, ACC>), dim3(tiles * chunks), dim3(64), 0, stream, a, rad, tiles, chunk, pool_rev());
         else hipLaunchKernelGGL((trace_pool_kernel<R, false, ACC>), dim3(tiles * chunks), dim3(64), 0, stream, a, rad, tiles, chunk, pool_rev());
-        hipLaunchKernelGGL(accumulate_kernel<R>, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream, a.c.sum,
-                           (const R*)rad, npix, ns);
+        hipLaunchKernelGGL(accumulate_kernel<R>, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, stream, a.im, a.c.sum,
+                           (const R*)rad, tiles, ns);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -237,9 +237,9 @@ hipError_t trace(rt_scene* sc, const rt_settings* s, const ImageParams& im, cons
 // the budget (RT_POOL_MB, default 32 GiB of the 288 GB HBM, at most 40 % of the free device memory),
 // else as many whole samples as fit (launch_trace then splits the samples over several launches).
 // Kept by the scene between renders.
-int ensure_pool(rt_scene* sc, const rt_settings* s, size_t n, int samples, Counters& c) {
-    if (!trace_uses_pool() || samples <= 0 || n == 0) return RT_OK;
-    const size_t per_sample = n * 3 * (s->precision == RT_PREC_F32 ? sizeof(float) : sizeof(double));
+int ensure_pool(rt_scene* sc, const rt_settings* s, int cw, int ch, int samples, Counters& c) {
+    if (!trace_uses_pool() || samples <= 0 || cw <= 0 || ch <= 0) return RT_OK;
+    const size_t per_sample = pool_sample_bytes(cw, ch, s->precision == RT_PREC_F32 ? sizeof(float) : sizeof(double));
     static size_t budget = 0;
     if (!budget) {
         const char* e = getenv("RT_POOL_MB");
@@ -402,7 +402,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     im.s_begin = std::max(im.s_begin, first);
     const int s0 = im.s_begin, s1 = std::max(im.s_end, s0);
     const int batch = s->batch_samples > 0 ? s->batch_samples : std::max(1, s1 - s0);
-    if (s->max_depth > 0 && (rc = ensure_pool(sc, s, n, std::min(batch, s1 - s0), c))) return rc;
+    if (s->max_depth > 0 && (rc = ensure_pool(sc, s, cw, ch, std::min(batch, s1 - s0), c))) return rc;
     sc->ckpt_pixels = n;
     sc->ckpt_done = s0;
     double kernel_ms = 0;
@@ -500,7 +500,7 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
     HIP_TRY(hipMemsetAsync(sc->total.p, 0, kTotalSlots * sizeof(unsigned long long), st));
     ImageParams im = image_params(s, cw, ch);
     Counters c{d_sum, nullptr, nullptr, sc->total.p, sc->total.p + kQueueSlot};
-    if (s->max_depth > 0 && (rc = ensure_pool(sc, s, (size_t)cw * ch, im.s_end - im.s_begin, c))) return rc;
+    if (s->max_depth > 0 && (rc = ensure_pool(sc, s, cw, ch, im.s_end - im.s_begin, c))) return rc;
     HIP_TRY(hipEventRecord(sc->ev[0], st));
     HIP_TRY(trace(sc, s, im, c, st));
     HIP_TRY(hipEventRecord(sc->ev[1], st));

@@ -1,7 +1,7 @@
 """Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes into profiles/pmc_<workload>_<prec>.json (HBM bytes
-per trace launch), applying MI355X_MICROARCH.md's gfx950 correction: FETCH_SIZE reports 1/2 of the
+per trace step: the sum over the listed kernels of each one's per-launch average), applying MI355X_MICROARCH.md's gfx950 correction: FETCH_SIZE reports 1/2 of the
 bytes of a wide coalesced read stream (x2), WRITE_SIZE is exact; both are in KiB.
-usage: python scripts/pmc_summary.py FETCH.csv WRITE.csv OUT.json [kernel-substring]"""
+usage: python scripts/pmc_summary.py FETCH.csv WRITE.csv OUT.json [kernel-substring[,kernel-substring...]]"""
 import csv
 import json
 import sys
@@ -14,9 +14,16 @@ def per_launch(path, counter, kernel):
 
 
 fetch_csv, write_csv, out = sys.argv[1:4]
-kernel = sys.argv[4] if len(sys.argv) > 4 else "trace_kernel"
-f_kib, nf = per_launch(fetch_csv, "FETCH_SIZE", kernel)
-w_kib, nw = per_launch(write_csv, "WRITE_SIZE", kernel)
+kernel = sys.argv[4] if len(sys.argv) > 4 else "trace_pool_kernel,accumulate_kernel"
+f_kib = w_kib = 0.0
+nf, nw = [], []
+for k in kernel.split(","):
+    f, n = per_launch(fetch_csv, "FETCH_SIZE", k)
+    f_kib += f
+    nf.append(n)
+    w, n = per_launch(write_csv, "WRITE_SIZE", k)
+    w_kib += w
+    nw.append(n)
 fetch = 2 * f_kib * 1024
 write = w_kib * 1024
 json.dump({"kernel": kernel, "launches": [nf, nw], "FETCH_SIZE_KiB": f_kib, "WRITE_SIZE_KiB": w_kib,

@@ -12,4 +12,4 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/fetch -
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/write -o run -- python3 bench.py --no-cpu-baseline --no-end-to-end --steps 1 --warmup 0 "$@" > $out/write.log 2>&1 || exit $?
 f=$(find $out/fetch -name '*counter_collection.csv' | head -1)
 w=$(find $out/write -name '*counter_collection.csv' | head -1)
-python3 scripts/pmc_summary.py "$f" "$w" $out/pmc.json trace_kernel
+python3 scripts/pmc_summary.py "$f" "$w" $out/pmc.json trace_pool_kernel,accumulate_kernel
