@@ -57,6 +57,29 @@ RT_HD void start_sample(const SceneView<R>& sc, const ImageParams& im, int i, in
     }
 }
 
+// x^5 for Schlick's approximation (materials.js:79-83, Math.pow(1 - cosine, 5)), correctly rounded.
+// V8's Math.pow (fdlibm) and glibc's pow return the correctly rounded x^5 for these arguments; the
+// device pow (ocml, <= 1 ulp) costs ~100 binary64 instructions and is not always correctly rounded.
+// Here x^2, x^4, x^5 are carried as unevaluated sums hi + lo (error-free products by FMA): the pair
+// approximates x^5 to ~2^-100 relative, so the single final rounding gives RN(x^5) unless x^5 lies
+// within 2^-100 of a rounding midpoint.  10 binary64 ops; exact for x = 0 and x = 1.  Checked against
+// libm pow bit for bit (tests/test_hostcheck.py::test_pow5_correctly_rounded).  RT_POW5 = 0: device pow
+// (A/B).  Only for 0 <= x <= 2 (no overflow/underflow concerns: x is 0 or >= 2^-53).
+#ifndef RT_POW5
+#define RT_POW5 1
+#endif
+template <class R>
+RT_HD R pow5_rn(R x) {
+#if RT_POW5
+    const R p = x * x, pe = fma(x, x, -p);                 // x^2 = p + pe exactly
+    const R q = p * p, qe = fma(p, p, -q) + (R)2 * (p * pe); // x^4 ~ q + qe
+    const R r = q * x, re = fma(q, x, -r) + qe * x;          // x^5 ~ r + re
+    return r + re;
+#else
+    return pow(x, (R)5);
+#endif
+}
+
 // Scatter at a non-emissive hit (materials.js:20-83).  Returns false when Metal absorbs.
 template <class R>
 RT_HD bool scatter(const MatRec<R>& m, const Hit<R>& h, V3<R> d, Rng<R>& g, V3<R>& nd, V3<R>& att) {
@@ -79,7 +102,7 @@ RT_HD bool scatter(const MatRec<R>& m, const Hit<R>& h, V3<R> d, Rng<R>& g, V3<R
     if (!reflect_it) {                                                        // random drawn only if it can refract
         R r0 = ((R)1 - ratio) / ((R)1 + ratio);
         r0 = r0 * r0;
-        R refl = r0 + ((R)1 - r0) * pow((R)1 - cos_t, (R)5);
+        R refl = r0 + ((R)1 - r0) * pow5_rn((R)1 - cos_t);
         reflect_it = refl > g.next();
     }
     if (reflect_it) {

@@ -249,3 +249,8 @@ extern "C" int ptc_work(const rt_scene_desc* d, const rt_settings* s, double* ou
         }
     return 0;
 }
+
+// pow5_rn (pt_path.h) on the host, for the comparison with libm pow (TEST TOOL)
+extern "C" void ptc_pow5(const double* x, double* out, long long n) {
+    for (long long i = 0; i < n; ++i) out[i] = rt::pow5_rn<double>(x[i]);
+}
