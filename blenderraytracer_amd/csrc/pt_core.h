@@ -471,6 +471,9 @@ typedef float rt_f2 __attribute__((ext_vector_type(2)));
 #ifndef RT_WALK_IFIF
 #define RT_WALK_IFIF 0            // 1: one step (node, or leaf + pop) per loop iteration
 #endif
+#ifndef RT_WALK_SPEC
+#define RT_WALK_SPEC 0            // 1: leaves parked and tested together (speculative traversal)
+#endif
 #ifndef RT_BVH_WHILE_WHILE
 #define RT_BVH_WHILE_WHILE 0
 #endif
@@ -599,6 +602,41 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
             return false;
 #endif
         };
+#if RT_WALK_SPEC && defined(__HIP_DEVICE_COMPILE__)
+        // Postponed leaves (speculative traversal): a lane that reaches a leaf parks it in `pend` and
+        // goes on walking inner nodes; the parked leaves are tested together once no lane of the
+        // wave is still looking for one (a lane that reaches a second leaf waits for that).  The
+        // closest hit does not depend on the visiting order (comment above `better`); a stale tl only
+        // visits more nodes, never fewer, so the result is bit-identical.
+        int pend = 0;                  // parked leaf reference (< 0), 0 = none
+        bool walking = true;
+        for (;;) {
+#if RT_PROFILE
+            ++w.lane_trips;
+            if ((int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) ++w.wave_trips;
+#endif
+            if (walking) {
+                if (cur >= 0) {
+                    RT_COUNT(++w.nodes);
+#if RT_BVH_UNIFORM
+                    const int first = __builtin_amdgcn_readfirstlane(cur);
+                    const bool down = __ballot(cur != first) == 0 ? step(wide[first]) : step(wide[cur]);
+#else
+                    const bool down = step(wide[cur]);
+#endif
+                    if (!down && !pop()) walking = false;
+                } else if (pend == 0) {
+                    pend = cur;
+                    if (!pop()) walking = false;
+                }
+            }
+            if (__ballot(walking && pend == 0) == 0 && pend != 0) {   // no lane still looking for a leaf
+                leaf(~pend);
+                pend = 0;
+            }
+            if (!walking && pend == 0) break;
+        }
+#else
         for (;;) {
 #if RT_PROFILE && defined(__HIP_DEVICE_COMPILE__)
             ++w.lane_trips;                       // the first active lane counts the wave's iteration
@@ -628,6 +666,7 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
             }
             if (!down && !pop()) break;
         }
+#endif  // RT_WALK_SPEC
 #endif
     } else {
         int ni = 0;
