@@ -101,6 +101,20 @@ def load_traffic(workload, precision):
     return None
 
 
+# VALU issue ceiling: 256 CUs x 4 SIMD-32s, a wave64 VALU instruction holds its SIMD for 2 cycles (a
+# binary64 one for 4: FP64 vector is half the FP32 rate) at 2.4 GHz (MI355X_MICROARCH.md)
+VALU_ISSUE_PEAK_GSLOTS = 256 * 4 * 2.4 / 2
+
+
+def load_sq(workload, precision):
+    """SQ counters of one trace step (profiles/sq_<workload>_<prec>.json, scripts/profile_round.sh)."""
+    p = os.path.join(ROOT, "profiles", f"sq_{workload}_{precision}.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return None
+
+
 def main():
     args = parse()
     cfg = CONFIGS[args.config]
@@ -172,6 +186,17 @@ def main():
             flops = seg_launch * flops_per_segment
         rank_samples = cfg["w"] * cfg["h"] * (job.range[1] - job.range[0])
         traffic = load_traffic(args.config, args.precision)
+        sq = load_sq(args.config, args.precision)
+        issue = None
+        if sq and world == 1:
+            slots = sq["valu_issue_slots"]
+            gslots = slots / (k_ms * 1e-3) / 1e9
+            issue = {"valu_insts_per_launch": sq["counters"]["SQ_INSTS_VALU"], "issue_slots_per_launch": slots,
+                     "achieved": round(gslots, 1), "peak": VALU_ISSUE_PEAK_GSLOTS,
+                     "unit": "G issue slots/s (wave64 VALU instruction = 1 slot, binary64 = 2)",
+                     "frac": round(gslots / VALU_ISSUE_PEAK_GSLOTS, 4),
+                     "lane_utilization": round(sq["valu_lane_utilization"], 4),
+                     "source": f"profiles/sq_{args.config}_{args.precision}.json (rocprofv3 SQ counters) / this run's kernel_ms"}
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -196,6 +221,7 @@ def main():
             "valu": {"achieved": round(flops / (k_ms * 1e-3) / 1e12, 3), "peak": VALU_PEAK_TFLOPS[args.precision],
                      "unit": "TFLOP/s", "frac": round(flops / (k_ms * 1e-3) / 1e12 / VALU_PEAK_TFLOPS[args.precision], 4),
                      "flops_per_segment": round(flops / seg_launch, 2)},
+            "valu_issue": issue,
             "segments_per_sample": round(seg_launch / rank_samples, 4),
             "kernel_msamples_per_s": round(rank_samples / (k_ms * 1e-3) / 1e6, 3),
             "cpu_baseline": cpu,

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <string.h>
 
 // Path code is __host__ __device__ so that tests/hostcheck can run the kernel's exact per-lane
 // logic on the CPU (test infrastructure only; librt_hip.so has no host execution path).
@@ -91,6 +92,20 @@ struct BvhNode { float lo[3]; int skip; float hi[3]; int fc; };
 // Bounds interleaved by child (lo[axis][child]) so both children's planes of an axis form one float2:
 // the slab test is 6 packed FMAs (v_pk_fma_f32) per node.
 struct Bvh2Node { float lo[3][2]; float hi[3][2]; int child[2]; int pad[2]; };
+// The same node with the child boxes rounded OUTWARD to binary16 (scene_pack.h:to_half_node): 32 B, so
+// a lane's node read is two 16-B loads instead of four (the walk is bound by the L1 -> VGPR data path,
+// TD busy ~0.8 of cycles).  A box only grows (by <= 2^-11 of its coordinates), so the ordered walk
+// still never culls a node holding a better primitive (bvh_conservative_bound): results unchanged.
+// Coordinates beyond the binary16 range round to +-inf (the node is then always entered).
+struct Bvh2NodeH { _Float16 lo[3][2]; _Float16 hi[3][2]; int child[2]; };
+#ifndef RT_BVH_HALF
+#define RT_BVH_HALF 0
+#endif
+#if RT_BVH_HALF
+using WideNode = Bvh2NodeH;
+#else
+using WideNode = Bvh2Node;
+#endif
 // Four-child node (128 B), collapsed from the binary tree: children in pairs (0,1), (2,3) for the
 // packed slab test; child RT_CHILD_EMPTY never hits.  Stack bound checked at build (scene_pack.h).
 struct Bvh4Node { float lo[3][4]; float hi[3][4]; int child[4]; int pad[4]; };
@@ -134,8 +149,8 @@ struct SceneView {
     const BvhNode* tri_nodes;
     int num_tri_nodes;
     const TriLeaf<R>* bvh_tri_leaf;
-    const Bvh2Node* sphere_wide;   // two-child nodes of the two trees (preorder)
-    const Bvh2Node* tri_wide;
+    const WideNode* sphere_wide;   // two-child nodes of the two trees (preorder)
+    const WideNode* tri_wide;
     int num_sphere_wide, num_tri_wide;
     const Bvh4Node* sphere_wide4;  // four-child collapse of the two trees (preorder)
     const Bvh4Node* tri_wide4;
@@ -509,11 +524,35 @@ RT_HD void bvh_node2_hit(const Bvh2Node& n, const BvhRay& r, float tlimit, bool&
     h1 = t1 <= f1;
 }
 
+// Half-precision node: the binary16 bounds widen exactly to binary32 inside the FMA (v_fma_mix_f32).
+RT_HD void bvh_node2_hit(const Bvh2NodeH& n, const BvhRay& r, float tlimit, bool& h0, bool& h1, float& t0,
+                         float& t1) {
+    // both 16-B halves of the node in flight at once (the compiler otherwise waits for the first
+    // before issuing the second: two memory round trips per node)
+    uint32_t q[6];
+    memcpy(q, &n, sizeof q);
+    for (int i = 0; i < 6; ++i) RT_KEEP(q[i]);
+    auto lo = [&](int k, int c) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(q[k] >> (16 * c))); };
+    auto hi = [&](int k, int c) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(q[3 + k] >> (16 * c))); };
+    float a[3][2], b[3][2];
+    for (int k = 0; k < 3; ++k)
+        for (int c = 0; c < 2; ++c) {
+            a[k][c] = __builtin_fmaf(lo(k, c), r.inv[k], -r.slo[k]);
+            b[k][c] = __builtin_fmaf(hi(k, c), r.inv[k], -r.shi[k]);
+        }
+    t0 = fmaxf(fmaxf(fminf(a[0][0], b[0][0]), fminf(a[1][0], b[1][0])), fmaxf(fminf(a[2][0], b[2][0]), 0.0f));
+    t1 = fmaxf(fmaxf(fminf(a[0][1], b[0][1]), fminf(a[1][1], b[1][1])), fmaxf(fminf(a[2][1], b[2][1]), 0.0f));
+    const float f0 = fminf(fminf(fmaxf(a[0][0], b[0][0]), fmaxf(a[1][0], b[1][0])), fminf(fmaxf(a[2][0], b[2][0]), tlimit));
+    const float f1 = fminf(fminf(fmaxf(a[0][1], b[0][1]), fmaxf(a[1][1], b[1][1])), fminf(fmaxf(a[2][1], b[2][1]), tlimit));
+    h0 = t0 <= f0;
+    h1 = t1 <= f1;
+}
+
 // Walk one BVH and call leaf(fc) for every leaf whose box the ray reaches before the current best.
 // WIDE: ordered walk over Bvh2Node (both child boxes per 64-B node, nearer child first, the other
 // pushed on the lane's stack); otherwise the stackless preorder walk over BvhNode skip links.
 template <bool WIDE, class Leaf>
-RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const BvhRay& br, const float& tl,
+RT_HD void bvh_walk(const BvhNode* nodes, int count, const WideNode* wide, const BvhRay& br, const float& tl,
                     BvhStack stk, Work& w, Leaf&& leaf) {
     if constexpr (WIDE) {
 #if RT_BVH_WHILE_WHILE
@@ -524,7 +563,7 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
         bool live = true;
         while (live) {
             while (cur >= 0) {
-                const Bvh2Node n = wide[cur];
+                const WideNode n = wide[cur];
                 RT_COUNT(++w.nodes);
                 float t0, t1;
                 bool h0, h1;
@@ -573,7 +612,7 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
             return true;
         };
         // true: descend to the new cur
-        auto step = [&](const Bvh2Node& n) -> bool {
+        auto step = [&](const WideNode& n) -> bool {
             float t0, t1;
             bool h0, h1;
             bvh_node2_hit(n, br, tl, h0, h1, t0, t1);

@@ -98,7 +98,7 @@ struct DeviceScene {
     DevBuf<BvhNode> sphere_nodes, tri_nodes;
     DevBuf<SphereLeaf<R>> bvh_sphere_leaf;
     DevBuf<TriLeaf<R>> bvh_tri_leaf;
-    DevBuf<Bvh2Node> sphere_wide, tri_wide;
+    DevBuf<WideNode> sphere_wide, tri_wide;
     DevBuf<Bvh4Node> sphere_wide4, tri_wide4;
     SceneView<R> view{};
     void release() {

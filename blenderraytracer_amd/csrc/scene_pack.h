@@ -23,7 +23,7 @@ struct HostScene {   // precision-independent staging, binary64 as packed by the
     std::vector<double> tri_verts;                                // v0, v1, v2 as given (BVH bounds)
     std::vector<BvhNode> sphere_bvh, tri_bvh;                     // built by build_bvhs()
     std::vector<int> sphere_bvh_prims, tri_bvh_prims;
-    std::vector<Bvh2Node> sphere_wide, tri_wide;                  // the same trees, two-child nodes
+    std::vector<WideNode> sphere_wide, tri_wide;                  // the same trees, two-child nodes
     int bvh_depth = 0;                                            // deepest leaf of either tree
     std::vector<Bvh4Node> sphere_wide4, tri_wide4;                // four-child collapse of the trees
     int bvh4_stack = 0;                                           // their worst traversal-stack use
@@ -334,6 +334,45 @@ inline std::vector<Bvh2Node> make_wide(const std::vector<BvhNode>& t) {
     return out;
 }
 
+// binary32 -> binary16 rounded toward +inf (up) or -inf (down): the result bounds x on that side
+inline _Float16 f16_toward(float x, bool up) {
+    _Float16 h = (_Float16)x;
+    const float back = (float)h;
+    if (x != x || (up ? back >= x : back <= x)) return h;
+    uint16_t u;
+    memcpy(&u, &h, 2);
+    if ((u & 0x7FFF) == 0) u = up ? 0x0001 : 0x8001;            // +-0 -> smallest subnormal
+    else if (!(u & 0x8000)) u = up ? (uint16_t)(u + 1) : (uint16_t)(u - 1);
+    else u = up ? (uint16_t)(u - 1) : (uint16_t)(u + 1);
+    memcpy(&h, &u, 2);
+    return h;
+}
+
+// Bvh2Node -> Bvh2NodeH: lower bounds rounded down, upper bounds up (pt_core.h)
+inline Bvh2NodeH to_half_node(const Bvh2Node& n) {
+    Bvh2NodeH h{};
+    for (int a = 0; a < 3; ++a)
+        for (int c = 0; c < 2; ++c) {
+            h.lo[a][c] = f16_toward(n.lo[a][c], false);
+            h.hi[a][c] = f16_toward(n.hi[a][c], true);
+        }
+    h.child[0] = n.child[0];
+    h.child[1] = n.child[1];
+    return h;
+}
+
+inline std::vector<WideNode> make_wide_nodes(const std::vector<BvhNode>& t) {
+    const std::vector<Bvh2Node> w = make_wide(t);
+#if RT_BVH_HALF
+    std::vector<WideNode> out;
+    out.reserve(w.size());
+    for (const Bvh2Node& n : w) out.push_back(to_half_node(n));
+    return out;
+#else
+    return w;
+#endif
+}
+
 // preorder BvhNode tree -> Bvh4Node array (root first, preorder): each four-child node takes its
 // binary node's two children and opens the inner child of largest surface area until it has four.
 // Returns the largest traversal-stack use of the ordered walk (a node pushes up to children-1
@@ -421,8 +460,8 @@ inline void build_bvhs(HostScene& hs) {
     hs.bvh_depth = std::max(hs.bvh_depth, tb.max_depth);
     hs.tri_bvh = std::move(tb.nodes);
     hs.tri_bvh_prims = std::move(tb.order);
-    hs.sphere_wide = make_wide(hs.sphere_bvh);
-    hs.tri_wide = make_wide(hs.tri_bvh);
+    hs.sphere_wide = make_wide_nodes(hs.sphere_bvh);
+    hs.tri_wide = make_wide_nodes(hs.tri_bvh);
     hs.bvh4_stack = std::max(make_wide4(hs.sphere_bvh, hs.sphere_wide4), make_wide4(hs.tri_bvh, hs.tri_wide4));
 }
 
