@@ -36,8 +36,9 @@ constexpr int kTileW = RT_WG_WAVES >= 2 ? 16 : 8;
 constexpr int kTileH = RT_WG_WAVES == 4 ? 16 : 8;
 
 #ifndef RT_MIN_WAVES_PER_SIMD
-#define RT_MIN_WAVES_PER_SIMD 8   // 64 VGPRs: latency-bound loop, 8 waves/SIMD measured fastest
-#endif
+#define RT_MIN_WAVES_PER_SIMD 6   // brute force: 80 VGPRs.  At 8 waves (64 VGPRs) the binary64 pool kernel
+#endif                            // spills 300 B/lane: Cornell f64 5175 (8) / 6730 (4) / 6830 (6) Msamples/s,
+                                  // f32 9274 (8) / 9680 (4) / 9978 (6)
 
 #ifndef RT_BVH_WAVES_PER_SIMD
 #define RT_BVH_WAVES_PER_SIMD 4   // binary64 BVH walk: 128 VGPRs (measured 3/4/5 waves: 3861/4065/3287)
