@@ -163,7 +163,7 @@ void trace_pool_kernel(const TraceArgs<R> args, R* __restrict__ rad, const int t
     }
     const LdsSpheres lds{nullptr};
     const int lane = threadIdx.x;
-    const int ci = blockIdx.x / tiles, tile = rev ? tiles - 1 - (int)(blockIdx.x % tiles) : blockIdx.x % tiles;
+    const int ci = blockIdx.x / tiles, tile = (rev & 1) ? tiles - 1 - (int)(blockIdx.x % tiles) : blockIdx.x % tiles;
     const int tiles_x = (im.cw + 7) / 8;
     const int tx0 = (tile % tiles_x) * 8, ty0 = (tile / tiles_x) * 8;
     const int vw = min(8, im.cw - tx0), nv = vw * min(8, im.ch - ty0);   // valid pixels of the tile
@@ -179,7 +179,8 @@ void trace_pool_kernel(const TraceArgs<R> args, R* __restrict__ rad, const int t
     V3<R> o, d, T;
     auto begin_item = [&](const uint32_t k) {
         uint32_t sr;
-        if (nv == 64) { m = k & 63; sr = k >> 6; }
+        if (rev & 2) { const uint32_t cs = (uint32_t)(se - sb); m = k / cs; sr = k - m * cs; }   // A/B: pixel-major
+        else if (nv == 64) { m = k & 63; sr = k >> 6; }
         else { sr = k / (uint32_t)nv; m = k - sr * (uint32_t)nv; }
         const int px = tx0 + (int)(m % (uint32_t)vw), py = ty0 + (int)(m / (uint32_t)vw);
         const int row = im.y0 + py;
@@ -260,12 +261,13 @@ bool trace_uses_pool() {
     return v == 1;
 }
 
-// tile order within a chunk (RT_POOL_ORDER=rev: last tile first; A/B runs)
+// A/B orders (RT_POOL_ORDER): rev = last tile first; pixel = a wave deals its items pixel-major (the
+// samples of one pixel consecutively) instead of sample-major
 static int pool_rev() {
     static int v = -1;
     if (v == -1) {
         const char* e = getenv("RT_POOL_ORDER");
-        v = e && e[0] == 'r';
+        v = !e ? 0 : (e[0] == 'r' ? 1 : (e[0] == 'p' ? 2 : 0));
     }
     return v;
 }
