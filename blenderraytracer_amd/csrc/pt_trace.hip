@@ -179,8 +179,7 @@ void trace_pool_kernel(const TraceArgs<R> args, R* __restrict__ rad, const int t
     V3<R> o, d, T;
     auto begin_item = [&](const uint32_t k) {
         uint32_t sr;
-        if (rev & 2) { const uint32_t cs = (uint32_t)(se - sb); m = k / cs; sr = k - m * cs; }   // A/B: pixel-major
-        else if (nv == 64) { m = k & 63; sr = k >> 6; }
+        if (nv == 64) { m = k & 63; sr = k >> 6; }
         else { sr = k / (uint32_t)nv; m = k - sr * (uint32_t)nv; }
         const int px = tx0 + (int)(m % (uint32_t)vw), py = ty0 + (int)(m / (uint32_t)vw);
         const int row = im.y0 + py;
@@ -261,13 +260,12 @@ bool trace_uses_pool() {
     return v == 1;
 }
 
-// A/B orders (RT_POOL_ORDER): rev = last tile first; pixel = a wave deals its items pixel-major (the
-// samples of one pixel consecutively) instead of sample-major
+// A/B tile order (RT_POOL_ORDER=rev: last tile first within each chunk)
 static int pool_rev() {
     static int v = -1;
     if (v == -1) {
         const char* e = getenv("RT_POOL_ORDER");
-        v = !e ? 0 : (e[0] == 'r' ? 1 : (e[0] == 'p' ? 2 : 0));
+        v = e && e[0] == 'r';
     }
     return v;
 }
