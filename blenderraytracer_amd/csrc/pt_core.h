@@ -15,6 +15,17 @@
 // Path code is __host__ __device__ so that tests/hostcheck can run the kernel's exact per-lane
 // logic on the CPU (test infrastructure only; librt_hip.so has no host execution path).
 #define RT_HD __host__ __device__ __forceinline__
+// Code the hot loop rarely or never runs (hdri / procedural backgrounds, stochastic AA) is kept out of
+// line on the device, so it does not take part in the trace kernel's register allocation.
+#ifndef RT_COLD_BG
+#define RT_COLD_BG 1               // RTOW +1.2 %, mesh50k +0.8 %, Cornell -1.5 % (DESIGN.md)
+#endif
+#if RT_COLD_BG && defined(__HIP_DEVICE_COMPILE__)
+#define RT_COLD __attribute__((noinline))
+#else
+#define RT_COLD
+#endif
+#define RT_COLD_HD __host__ __device__ RT_COLD
 
 namespace rt {
 
@@ -1006,14 +1017,6 @@ __host__ __device__ R perlin(const int* p, R x, R y, R z) {
 // Backgrounds the hot loop rarely or never takes (hdri, procedural sky with Perlin noise) are kept
 // out of line (RT_COLD_BG): their code then does not take part in the trace kernel's register
 // allocation.
-#ifndef RT_COLD_BG
-#define RT_COLD_BG 1               // RTOW +1.2 %, mesh50k +0.8 %, Cornell -1.5 % (DESIGN.md)
-#endif
-#if RT_COLD_BG && defined(__HIP_DEVICE_COMPILE__)
-#define RT_COLD __attribute__((noinline))
-#else
-#define RT_COLD
-#endif
 
 template <class R>
 __host__ __device__ RT_COLD V3<R> background_hdri(const SceneView<R>& sc, V3<R> d) {             // world.js:74-110

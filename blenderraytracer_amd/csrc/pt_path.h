@@ -22,6 +22,19 @@ struct ImageParams {
     uint32_t seedm;            // seed_mix(seed)
 };
 
+// Stochastic AA offsets (ray-tracer.js:136-141): sqrt, cos and sin in binary64 are long code that
+// the default supersampling never runs, so they stay out of line (RT_COLD, pt_core.h).  Arguments and
+// result by value: no local's address escapes into the call.
+template <class R> struct AaUv { R u, v; };
+template <class R>
+RT_COLD_HD AaUv<R> stochastic_uv(uint32_t key, int i, int j, int width, int height) {
+    Rng<R> g{key, 0};
+    R r1 = g.next(), r2 = g.next();
+    R ox = sqrt(r1) * cos((R)2 * (R)3.141592653589793 * r2);
+    R oy = sqrt(r1) * sin((R)2 * (R)3.141592653589793 * r2);
+    return AaUv<R>{((R)i + (R)0.5 + ox * (R)0.5) / (R)width, ((R)j + (R)0.5 + oy * (R)0.5) / (R)height};
+}
+
 template <class R>
 RT_HD void start_sample(const SceneView<R>& sc, const ImageParams& im, int i, int j, uint32_t pkey, int s, Rng<R>& g,
                         V3<R>& o, V3<R>& d) {
@@ -29,11 +42,10 @@ RT_HD void start_sample(const SceneView<R>& sc, const ImageParams& im, int i, in
     g.k = 0;
     R u, v;                                                                   // ray-tracer.js:125-149
     if (im.aa_mode == 1) {
-        R r1 = g.next(), r2 = g.next();
-        R ox = sqrt(r1) * cos((R)2 * (R)3.141592653589793 * r2);
-        R oy = sqrt(r1) * sin((R)2 * (R)3.141592653589793 * r2);
-        u = ((R)i + (R)0.5 + ox * (R)0.5) / (R)im.width;
-        v = ((R)j + (R)0.5 + oy * (R)0.5) / (R)im.height;
+        const AaUv<R> uv = stochastic_uv<R>(g.key, i, j, im.width, im.height);
+        u = uv.u;
+        v = uv.v;
+        g.k = 2;
     } else if (im.aa_mode == 0) {
         u = ((R)i + g.next()) / (R)im.width;
         v = ((R)j + g.next()) / (R)im.height;
