@@ -559,6 +559,21 @@ RT_HD void bvh_node2_hit(const Bvh2NodeH& n, const BvhRay& r, float tlimit, bool
     h1 = t1 <= f1;
 }
 
+#ifndef RT_BVH_BUFFER
+#define RT_BVH_BUFFER 1           // per-lane node reads as buffer loads (32-bit offsets): RTOW +1.4 %, f32 +2 %
+#endif
+#if RT_BVH_BUFFER && defined(__HIP_DEVICE_COMPILE__)
+typedef unsigned int rt_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ WideNode load_wide(__amdgpu_buffer_rsrc_t rs, int i) {
+    const int off = i * (int)sizeof(WideNode);
+    rt_u4 q[sizeof(WideNode) / 16];
+    for (int k = 0; k < (int)(sizeof(WideNode) / 16); ++k) q[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * k, 0, 0);
+    WideNode n;
+    memcpy(&n, q, sizeof n);
+    return n;
+}
+#endif
+
 // Walk one BVH and call leaf(fc) for every leaf whose box the ray reaches before the current best.
 // WIDE: ordered walk over Bvh2Node (both child boxes per 64-B node, nearer child first, the other
 // pushed on the lane's stack); otherwise the stackless preorder walk over BvhNode skip links.
@@ -599,6 +614,9 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const WideNode* wide, const
         }
 #else
         int sp = 0, cur = 0;
+#if RT_BVH_BUFFER && RT_BVH_UNIFORM && defined(__HIP_DEVICE_COMPILE__)
+        const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)wide, (short)0, 0x7FFFFFFF, 0x00020000);
+#endif
 #if RT_STACK_TOP
         int top = RT_CHILD_EMPTY;   // never a node or leaf reference (leaves hold <= 15 primitives)
 #endif
@@ -704,7 +722,11 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const WideNode* wide, const
                 // every active lane at the same node (30 % of RTOW walk steps, 49 % on mesh50k): read
                 // it with scalar loads, which bypass the vector memory pipeline
                 const int first = __builtin_amdgcn_readfirstlane(cur);
+#if RT_BVH_BUFFER
+                down = __ballot(cur != first) == 0 ? step(wide[first]) : step(load_wide(wrs, cur));
+#else
                 down = __ballot(cur != first) == 0 ? step(wide[first]) : step(wide[cur]);
+#endif
 #else
                 down = step(wide[cur]);
 #endif
