@@ -562,16 +562,23 @@ RT_HD void bvh_node2_hit(const Bvh2NodeH& n, const BvhRay& r, float tlimit, bool
 #ifndef RT_BVH_BUFFER
 #define RT_BVH_BUFFER 1           // per-lane node reads as buffer loads (32-bit offsets): RTOW +1.4 %, f32 +2 %
 #endif
-#if RT_BVH_BUFFER && defined(__HIP_DEVICE_COMPILE__)
+#ifndef RT_LEAF_BUFFER
+#define RT_LEAF_BUFFER 0          // 1: leaf records read as buffer loads too
+#endif
+#if (RT_BVH_BUFFER || RT_LEAF_BUFFER) && defined(__HIP_DEVICE_COMPILE__)
 typedef unsigned int rt_u4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ WideNode load_wide(__amdgpu_buffer_rsrc_t rs, int i) {
-    const int off = i * (int)sizeof(WideNode);
-    rt_u4 q[sizeof(WideNode) / 16];
-    for (int k = 0; k < (int)(sizeof(WideNode) / 16); ++k) q[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * k, 0, 0);
-    WideNode n;
+// record i of a 16-B-multiple array behind a raw buffer descriptor (32-bit offset, no 64-bit address math)
+template <class T>
+__device__ __forceinline__ T load_rec(__amdgpu_buffer_rsrc_t rs, int i) {
+    static_assert(sizeof(T) % 16 == 0, "16-B records");
+    const int off = i * (int)sizeof(T);
+    rt_u4 q[sizeof(T) / 16];
+    for (int k = 0; k < (int)(sizeof(T) / 16); ++k) q[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * k, 0, 0);
+    T n;
     memcpy(&n, q, sizeof n);
     return n;
 }
+__device__ __forceinline__ WideNode load_wide(__amdgpu_buffer_rsrc_t rs, int i) { return load_rec<WideNode>(rs, i); }
 #endif
 
 // Walk one BVH and call leaf(fc) for every leaf whose box the ray reaches before the current best.
@@ -795,8 +802,15 @@ RT_HD void sphere_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R a, co
                        Closest<R>& b, float& tl, Work& w) {
     const int first = fc >> 4, end = first + (fc & 15);
     RT_COUNT(w.spheres += end - first);
+#if RT_LEAF_BUFFER && defined(__HIP_DEVICE_COMPILE__)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)sc.bvh_sphere_leaf, (short)0, 0x7FFFFFFF, 0x00020000);
+#endif
     for (int k = first; k < end; ++k) {
+#if RT_LEAF_BUFFER && defined(__HIP_DEVICE_COMPILE__)
+        SphereLeaf<R> L = load_rec<SphereLeaf<R>>(rs, k);
+#else
         SphereLeaf<R> L = sc.bvh_sphere_leaf[k];
+#endif
 #if RT_LEAF_PREFETCH
         RT_KEEP(L.s.cx); RT_KEEP(L.s.cy); RT_KEEP(L.s.cz); RT_KEEP(L.s.r2);
         RT_KEEP(L.id); RT_KEEP(L.obj); RT_KEEP(L.mat);
@@ -830,8 +844,15 @@ template <class R>
 RT_HD void tri_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R tmin, Closest<R>& b, float& tl, Work& w) {
     const int first = fc >> 4, end = first + (fc & 15);
     RT_COUNT(w.tris += end - first);
+#if RT_LEAF_BUFFER && defined(__HIP_DEVICE_COMPILE__)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)sc.bvh_tri_leaf, (short)0, 0x7FFFFFFF, 0x00020000);
+#endif
     for (int k = first; k < end; ++k) {
+#if RT_LEAF_BUFFER && defined(__HIP_DEVICE_COMPILE__)
+        TriLeaf<R> L = load_rec<TriLeaf<R>>(rs, k);
+#else
         TriLeaf<R> L = sc.bvh_tri_leaf[k];
+#endif
 #if RT_LEAF_PREFETCH
         RT_KEEP(L.t.v0x); RT_KEEP(L.t.e1x); RT_KEEP(L.t.e2x); RT_KEEP(L.t.nz);
         RT_KEEP(L.id); RT_KEEP(L.obj); RT_KEEP(L.mat);
