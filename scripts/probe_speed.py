@@ -1,5 +1,6 @@
 """Quick throughput probe: renders a workload at reduced spp in both precisions, prints Msamples/s.
 usage: python scripts/probe_speed.py [config] [spp] [precisions] [accel: auto|brute|bvh]"""
+import hashlib
 import os
 import sys
 import time
@@ -18,10 +19,11 @@ for prec in precs:
     rt = bench.make_tracer(cfg, prec, 1, 0, accel)
     rt.render()                                  # warm-up + upload
     t = time.perf_counter()
-    rt.render()
+    img = rt.render()
     dt = time.perf_counter() - t
     st = rt.last_stats
     n = cfg["w"] * cfg["h"] * spp
     print(f"{cfg_name} {cfg['w']}x{cfg['h']}x{spp} {prec} {accel}: wall {dt*1e3:.1f} ms, kernel {st.kernel_ms:.1f} ms, "
-          f"{n / (st.kernel_ms * 1e-3) / 1e6:.1f} Msamples/s (kernel), segments/sample {st.segments / n:.3f}", flush=True)
+          f"{n / (st.kernel_ms * 1e-3) / 1e6:.1f} Msamples/s (kernel), segments/sample {st.segments / n:.3f}, "
+          f"image md5 {hashlib.md5(img['rgba8'].tobytes()).hexdigest()[:12]}", flush=True)
     rt.close()
