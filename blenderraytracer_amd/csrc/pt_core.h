@@ -513,6 +513,21 @@ typedef float rt_f2 __attribute__((ext_vector_type(2)));
 #ifndef RT_BVH_PACKED
 #define RT_BVH_PACKED 1           // 0: twelve scalar FMAs (no duplicated {inv, inv} register pairs)
 #endif
+#ifndef RT_BVH_MINIMUM
+#define RT_BVH_MINIMUM 1
+#endif
+#if RT_BVH_MINIMUM && defined(__HIP_DEVICE_COMPILE__)
+// IEEE 754-2019 minimum / maximum (v_minimum3_f32 / v_maximum3_f32 on gfx950): unlike fminf / fmaxf
+// they need no canonicalized inputs, so the loop-carried ray limit is not re-canonicalized at every
+// node.  They differ from fminf / fmaxf only for NaN operands (propagated instead of dropped: a NaN
+// ray then enters no node, and no leaf could have given it a hit) and in ordering -0 below +0 (equal
+// under the <= / < tests below): same decisions
+#define RT_SLAB_MIN(a, b) __builtin_elementwise_minimum(a, b)
+#define RT_SLAB_MAX(a, b) __builtin_elementwise_maximum(a, b)
+#else
+#define RT_SLAB_MIN(a, b) fminf(a, b)
+#define RT_SLAB_MAX(a, b) fmaxf(a, b)
+#endif
 RT_HD void bvh_node2_hit(const Bvh2Node& n, const BvhRay& r, float tlimit, bool& h0, bool& h1, float& t0,
                          float& t1) {
     rt_f2 a[3], b[3];
@@ -527,10 +542,14 @@ RT_HD void bvh_node2_hit(const Bvh2Node& n, const BvhRay& r, float tlimit, bool&
         b[k] = rt_f2{__builtin_fmaf(n.hi[k][0], r.inv[k], -r.shi[k]), __builtin_fmaf(n.hi[k][1], r.inv[k], -r.shi[k])};
 #endif
     }
-    t0 = fmaxf(fmaxf(fminf(a[0].x, b[0].x), fminf(a[1].x, b[1].x)), fmaxf(fminf(a[2].x, b[2].x), 0.0f));
-    t1 = fmaxf(fmaxf(fminf(a[0].y, b[0].y), fminf(a[1].y, b[1].y)), fmaxf(fminf(a[2].y, b[2].y), 0.0f));
-    const float f0 = fminf(fminf(fmaxf(a[0].x, b[0].x), fmaxf(a[1].x, b[1].x)), fminf(fmaxf(a[2].x, b[2].x), tlimit));
-    const float f1 = fminf(fminf(fmaxf(a[0].y, b[0].y), fmaxf(a[1].y, b[1].y)), fminf(fmaxf(a[2].y, b[2].y), tlimit));
+#define MN RT_SLAB_MIN
+#define MX RT_SLAB_MAX
+    t0 = MX(MX(MN(a[0].x, b[0].x), MN(a[1].x, b[1].x)), MX(MN(a[2].x, b[2].x), 0.0f));
+    t1 = MX(MX(MN(a[0].y, b[0].y), MN(a[1].y, b[1].y)), MX(MN(a[2].y, b[2].y), 0.0f));
+    const float f0 = MN(MN(MX(a[0].x, b[0].x), MX(a[1].x, b[1].x)), MN(MX(a[2].x, b[2].x), tlimit));
+    const float f1 = MN(MN(MX(a[0].y, b[0].y), MX(a[1].y, b[1].y)), MN(MX(a[2].y, b[2].y), tlimit));
+#undef MN
+#undef MX
     h0 = t0 <= f0;
     h1 = t1 <= f1;
 }
