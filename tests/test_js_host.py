@@ -155,7 +155,10 @@ def test_js_gpu_render_matches_reference(gpu):
             assert np.mean(ld("rgba8", np.uint8).reshape(ch, cw, 4) == gc.load_array(name, "rgba8")) >= 0.9999
         r = summary["_render"]
         assert r["progress"][-1] == 1.0 and r["nonzero"]
-        # window.renderCancelled set in the 2nd of 4 progress callbacks (delivered asynchronously, so
-        # the worker may finish one more batch), then GpuRayTracer.resume(): the same image
+        # window.renderCancelled set in the 2nd of 4 progress callbacks, then GpuRayTracer.resume():
+        # the same image.  The callbacks reach the JS thread asynchronously, so a fast enough GPU
+        # finishes all batches before the cancel lands (samplesDone 8, resume then has nothing left);
+        # the deterministic cancel / checkpoint / resume check is test_gpu_parity.py's
+        # test_checkpoint_resume_is_bit_exact
         assert summary["_resume"]["equal"] is True
-        assert summary["_resume"]["samplesDone"] in (4, 6)
+        assert summary["_resume"]["samplesDone"] in (4, 6, 8)
