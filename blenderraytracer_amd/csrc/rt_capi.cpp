@@ -495,7 +495,11 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
     if (!rc) rc = check_accel(sc, s);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(sc->device));
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : sc->stream;
+    // NULL is the default (null) stream, as for rt_finalize_device: the caller's zeroing of d_sum and
+    // its reduce / epilogue on that stream are ordered with this trace (the scene's own non-blocking
+    // stream would not be: a zeroing enqueued on the default stream could run after the trace's
+    // accumulate pass)
+    hipStream_t st = (hipStream_t)hip_stream;
     HIP_TRY(sc->total.ensure(kTotalSlots));
     HIP_TRY(hipMemsetAsync(sc->total.p, 0, kTotalSlots * sizeof(unsigned long long), st));
     ImageParams im = image_params(s, cw, ch);

@@ -294,3 +294,18 @@ def test_sample_pool_bit_identical(gpu, tmp_path, env):
     other = _render_in_child(_POOL_SCRIPT, tmp_path / "other.npz", **env)
     for k in base.files:
         assert np.array_equal(base[k], other[k], equal_nan=True), k
+
+
+def test_sharded_step_matches_render(gpu):
+    """bench.py's device path (ShardedRender.step: d_sum zeroed on torch's stream, rt_trace_device,
+    rt_finalize_device, no synchronization in between) gives the host API's image frame after frame:
+    the zeroing, the trace and the epilogue run in stream order."""
+    import torch
+    from blenderraytracer_amd.distributed import ShardedRender
+    rt = _rtow(640, 360, 8, seed=3)
+    ref = rt.render(want=("rgba8",))["rgba8"]
+    job = ShardedRender(rt, device=torch.device("cuda", 0))
+    for _ in range(3):
+        job.step(stats=False)
+        torch.cuda.synchronize()
+        assert np.array_equal(job.rgba8.cpu().numpy().reshape(ref.shape), ref)
