@@ -270,19 +270,20 @@ static int pool_rev() {
     return v;
 }
 
-// Samples per pool wave: ~1.5 sqrt(ns), halved (>= 4) until the launch has >= 64k waves (4x the chip's
-// 16k wave slots).  Short waves shorten the frame's drain tail; long ones shorten each wave's own tail
-// (its last items finish at different times).  Measured best chunks, 1080p: RTOW 512 spp 24-32,
-// 64 spp 16; mesh50k 256 spp 12, 32 spp 8; Cornell 512^2 x 64 spp (4096 tiles) 4.
+// Samples per pool wave: ~1.5 sqrt(ns) (0.75 sqrt(ns) when the scene has a triangle BVH: its walks
+// vary more in length, so shorter waves pay), halved (>= 4) until the launch has >= 64k waves (4x the
+// chip's 16k wave slots).  Short waves shorten the frame's drain tail; long ones shorten each wave's
+// own tail (its last items finish at different times).  Measured best chunks, 1080p: RTOW 512 spp
+// 24-34, 64 spp 16; mesh50k 256 spp 12, 32 spp 8; Cornell 512^2 x 64 spp (4096 tiles) 4.
 // RT_POOL_CHUNK overrides (A/B runs).
-static int pool_chunk(int ns, int tiles) {
+static int pool_chunk(int ns, int tiles, bool tri_bvh) {
     static int v = -1;
     if (v == -1) {
         const char* e = getenv("RT_POOL_CHUNK");
         v = e ? std::max(1, atoi(e)) : 0;
     }
     if (v) return v;
-    int c = std::min(64, std::max(4, (int)(1.5 * std::sqrt((double)ns) + 0.5)));
+    int c = std::min(64, std::max(4, (int)((tri_bvh ? 0.75 : 1.5) * std::sqrt((double)ns) + 0.5)));
     while (c > 4 && (long long)tiles * ((ns + c - 1) / c) < 65536) c = std::max(4, c / 2);
     return c;
 }
@@ -294,7 +295,7 @@ static hipError_t launch_pool(const TraceArgs<R>& a0, bool count, hipStream_t st
     const size_t fit = a0.c.pool ? a0.c.pool_bytes / per_sample : 0;
     if (fit < 1) return hipErrorInvalidValue;
     const int ns_max = (int)std::min<size_t>(fit, (size_t)(im.s_end - im.s_begin));
-    const int tiles = ((im.cw + 7) / 8) * ((im.ch + 7) / 8), chunk = pool_chunk(ns_max, tiles);
+    const int tiles = ((im.cw + 7) / 8) * ((im.ch + 7) / 8), chunk = pool_chunk(ns_max, tiles, ACC >= ACC_BVH && a0.sc.num_tri_nodes > 0);
     R* rad = static_cast<R*>(a0.c.pool);
     for (int b = im.s_begin; b < im.s_end; b += ns_max) {
         TraceArgs<R> a = a0;
