@@ -103,32 +103,8 @@ struct BvhNode { float lo[3]; int skip; float hi[3]; int fc; };
 // Bounds interleaved by child (lo[axis][child]) so both children's planes of an axis form one float2:
 // the slab test is 6 packed FMAs (v_pk_fma_f32) per node.
 struct Bvh2Node { float lo[3][2]; float hi[3][2]; int child[2]; int pad[2]; };
-// The same node with the child boxes rounded OUTWARD to binary16 (scene_pack.h:to_half_node): 32 B, so
-// a lane's node read is two 16-B loads instead of four (the walk is bound by the L1 -> VGPR data path,
-// TD busy ~0.8 of cycles).  A box only grows (by <= 2^-11 of its coordinates), so the ordered walk
-// still never culls a node holding a better primitive (bvh_conservative_bound): results unchanged.
-// Coordinates beyond the binary16 range round to +-inf (the node is then always entered).
-struct Bvh2NodeH { _Float16 lo[3][2]; _Float16 hi[3][2]; int child[2]; };
-#ifndef RT_BVH_HALF
-#define RT_BVH_HALF 0
-#endif
-#if RT_BVH_HALF
-using WideNode = Bvh2NodeH;
-#else
-using WideNode = Bvh2Node;
-#endif
-// Four-child node (128 B), collapsed from the binary tree: children in pairs (0,1), (2,3) for the
-// packed slab test; child RT_CHILD_EMPTY never hits.  Stack bound checked at build (scene_pack.h).
-struct Bvh4Node { float lo[3][4]; float hi[3][4]; int child[4]; int pad[4]; };
-#define RT_CHILD_EMPTY ((int)0x80000000)
-#ifndef RT_BVH4_STACK
-#define RT_BVH4_STACK 36          // 36 KB of LDS per workgroup (mesh50k needs 35)
-#endif
-#ifndef RT_BVH4_SORT
-#define RT_BVH4_SORT 1            // 1: hit children fully sorted by entry distance; 0: nearest only
-#endif
 #ifndef RT_BVH_STACK
-#define RT_BVH_STACK 24           // 24 KB of LDS per 256-lane workgroup; trees up to ~16.7M primitives
+#define RT_BVH_STACK 24           // 6 KB of LDS per one-wave workgroup; trees up to ~16.7M primitives
 #endif
 
 template <class R>
@@ -160,11 +136,10 @@ struct SceneView {
     const BvhNode* tri_nodes;
     int num_tri_nodes;
     const TriLeaf<R>* bvh_tri_leaf;
-    const WideNode* sphere_wide;   // two-child nodes of the two trees (preorder)
-    const WideNode* tri_wide;
+    const Bvh2Node* sphere_wide;   // two-child nodes of the two trees (preorder)
+    const Bvh2Node* tri_wide;
     int num_sphere_wide, num_tri_wide;
-    const Bvh4Node* sphere_wide4;  // four-child collapse of the two trees (preorder)
-    const Bvh4Node* tri_wide4;
+    int stack_entries;             // deepest leaf of the two trees (>= 1): the ordered walk's stack bound
     // camera (camera.js:8-36 vectors, computed on the host in binary64)
     R cam_o[3], cam_llc[3], cam_h[3], cam_v[3], cam_u[3], cam_vv[3], cam_w[3];
     R lens_radius;
@@ -179,30 +154,11 @@ enum HitKind : int { HIT_NONE = -1, HIT_SPHERE = 0, HIT_PLANE = 1, HIT_BOX = 2, 
 template <class R>
 struct Closest { R t; int kind, idx, mat, obj; };   // obj: World.objects index (BVH mode only)
 
-// Filter records staged in LDS by the workgroup (pt_trace.hip), read by every lane at the same
-// address (broadcast ds_read_b128).
-struct LdsSpheres { const SphereFilter* rec; };
-
 #ifndef RT_SPHERE_UNROLL
 #define RT_SPHERE_UNROLL 16
 #endif
 #define RT_PRAGMA(x) _Pragma(#x)
 #define RT_UNROLL(n) RT_PRAGMA(unroll n)
-
-#ifndef RT_SPHERE_AWAY
-#define RT_SPHERE_AWAY 0          // A/B option: measured -2 % on RTOW f64 (the branch saves nothing
-#endif                            // unless every lane of the wave takes it)
-// sphere_away_shortcut.  A ray whose origin is outside the sphere (c >= 0) and that moves away from
-// its centre (hb > 0) has both computed roots <= 0 < tMin, so the test can stop before sqrt and the
-// two divisions with the same answer: root1 = (-hb - sq)/a < 0, and with Y = RN(a c) >= 0,
-// disc = RN(RN(hb^2) - Y) <= RN(hb^2), so sq = RN(sqrt(disc)) <= RN(sqrt(RN(hb^2))) = hb (in binary
-// floating point, RN(sqrt(RN(h^2))) = h while h^2 neither overflows nor underflows: hence the range
-// check), and root2 = RN(RN(sq - hb)/a) <= 0.  tmin > 0 is required (World.hit's 0.001).
-template <class R>
-RT_HD bool sphere_moving_away(R hb, R c) {
-    return RT_SPHERE_AWAY && c >= (R)0 && hb > (R)(sizeof(R) == 8 ? 1e-150 : 1e-18) &&
-           hb < (R)(sizeof(R) == 8 ? 1e150 : 1e18);
-}
 
 // Sphere.hit (geometry.js:15-45) folded into World.hit's strict-< acceptance, in R arithmetic.
 template <class R>
@@ -211,7 +167,6 @@ RT_HD void sphere_test_f64(const SceneView<R>& sc, V3<R> o, V3<R> d, R a, R tmin
     R ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
     R hb = ocx * d.x + ocy * d.y + ocz * d.z;
     R c = (ocx * ocx + ocy * ocy + ocz * ocz) - s.r2;
-    if (sphere_moving_away(hb, c)) return;
     R disc = hb * hb - a * c;
     if (disc < (R)0) return;
     R sq = sqrt(disc);
@@ -259,8 +214,8 @@ RT_HD bool sphere_filter_pass(const SphereFilter& s, const FilterRay& r) {
 // material index, taken at accept time — is wave-uniform (scalar loads, no LDS).  Only
 // (t, kind, index, material) is tracked; the hit record is rebuilt afterwards from (t, primitive),
 // which is exact because no primitive's chosen t depends on tMax.
-template <class R, bool LDS = false>
-RT_HD Closest<R> closest_hit(const SceneView<R>& sc, V3<R> o, V3<R> d, const LdsSpheres lds = LdsSpheres{nullptr}) {
+template <class R>
+RT_HD Closest<R> closest_hit(const SceneView<R>& sc, V3<R> o, V3<R> d) {
     const R tmin = (R)0.001;
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0};
     const R a = dot(d, d);
@@ -272,18 +227,10 @@ RT_HD Closest<R> closest_hit(const SceneView<R>& sc, V3<R> o, V3<R> d, const Lds
                 // |disc32 - disc64| (sphere_filter_bound); only spheres the filter cannot reject get
                 // the binary64 test below, so every decision is the f64 one, at ~f32 cost per miss.
                 const FilterRay fr = make_filter_ray(o, d);
-                if constexpr (LDS) {
 RT_UNROLL(RT_SPHERE_UNROLL)
-                    for (int i = run.begin; i < run.end; ++i) {
-                        if (!sphere_filter_pass(lds.rec[i], fr)) continue;
-                        sphere_test_f64(sc, o, d, a, tmin, i, b);
-                    }
-                } else {
-RT_UNROLL(RT_SPHERE_UNROLL)
-                    for (int i = run.begin; i < run.end; ++i) {
-                        if (!sphere_filter_pass(sc.sphere_filter[i], fr)) continue;
-                        sphere_test_f64(sc, o, d, a, tmin, i, b);
-                    }
+                for (int i = run.begin; i < run.end; ++i) {
+                    if (!sphere_filter_pass(sc.sphere_filter[i], fr)) continue;
+                    sphere_test_f64(sc, o, d, a, tmin, i, b);
                 }
                 continue;
             }
@@ -363,7 +310,6 @@ RT_HD bool sphere_candidate(const SphereRec<R>& s, V3<R> o, V3<R> d, R a, R tmin
     R ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
     R hb = ocx * d.x + ocy * d.y + ocz * d.z;
     R c = (ocx * ocx + ocy * ocy + ocz * ocz) - s.r2;
-    if (sphere_moving_away(hb, c)) return false;
     R disc = hb * hb - a * c;
     if (disc < (R)0) return false;
     R sq = sqrt(disc);
@@ -438,13 +384,9 @@ RT_HD bool bvh_node_hit(const BvhNode& n, const BvhRay& r, float tlimit) {
 struct Work {
     uint32_t nodes, spheres, tris;                // BVH nodes visited, sphere / triangle tests (stats)
     uint32_t lane_trips, wave_trips, uni_trips;   // RT_PROFILE: walk iterations per lane / per wave / uniform
-    uint32_t x[4];                                // RT_WORK_EXTRA (host experiments): leaf-test breakdown
 };
-#ifndef RT_WORK_EXTRA
-#define RT_WORK_EXTRA 0
-#endif
 #ifndef RT_BVH_COUNT
-#define RT_BVH_COUNT 1
+#define RT_BVH_COUNT 1            // 0 measured slower (-2 % RTOW, -9 % mesh50k: worse register allocation)
 #endif
 #if RT_BVH_COUNT
 #define RT_COUNT(x) (x)
@@ -456,67 +398,9 @@ struct Work {
 // GPU, strided by the workgroup size so a wave's accesses are conflict-free)
 struct BvhStack { int* base; int stride; };
 
-#ifndef RT_BVH_FMA
-#define RT_BVH_FMA 1
-#endif
-RT_HD bool bvh_box_hit(const float* bx, const BvhRay& r, float tlimit, float& tn) {
-#if RT_BVH_FMA
-    const float x0 = __builtin_fmaf(bx[0], r.inv[0], -r.slo[0]), x1 = __builtin_fmaf(bx[3], r.inv[0], -r.shi[0]);
-    const float y0 = __builtin_fmaf(bx[1], r.inv[1], -r.slo[1]), y1 = __builtin_fmaf(bx[4], r.inv[1], -r.shi[1]);
-    const float z0 = __builtin_fmaf(bx[2], r.inv[2], -r.slo[2]), z1 = __builtin_fmaf(bx[5], r.inv[2], -r.shi[2]);
-#else
-    const float x0 = (bx[0] - r.olo[0]) * r.inv[0], x1 = (bx[3] - r.ohi[0]) * r.inv[0];
-    const float y0 = (bx[1] - r.olo[1]) * r.inv[1], y1 = (bx[4] - r.ohi[1]) * r.inv[1];
-    const float z0 = (bx[2] - r.olo[2]) * r.inv[2], z1 = (bx[5] - r.ohi[2]) * r.inv[2];
-#endif
-    tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.0f));
-    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tlimit));
-    return tn <= tf;
-}
-
 typedef float rt_f2 __attribute__((ext_vector_type(2)));
 
-// RT_KEEP(x): make x live in a VGPR at this point of the program.  Used to pin a load that the
-// compiler would otherwise sink into a later branch (a dependent memory round trip) next to the
-// loads issued with it.  No-op on the host build.
 #if defined(__HIP_DEVICE_COMPILE__)
-#define RT_KEEP(x) asm("" : "+v"(x))   // not volatile: a volatile asm would count as a memory clobber
-                                        // and cost the walk its scalar node loads
-#else
-#define RT_KEEP(x) ((void)0)
-#endif
-#ifndef RT_NODE_PREFETCH
-#define RT_NODE_PREFETCH 1        // child indices loaded with the child boxes (one round trip per node)
-#endif
-#ifndef RT_LEAF_PREFETCH
-#define RT_LEAF_PREFETCH 0        // a leaf record's filter, geometry and keys loaded together
-#endif
-#ifndef RT_STACK_TOP
-#define RT_STACK_TOP 0            // the most recently pushed node kept in a register
-#endif
-#ifndef RT_WALK_IFIF
-#define RT_WALK_IFIF 0            // 1: one step (node, or leaf + pop) per loop iteration
-#endif
-#ifndef RT_WALK_SPEC
-#define RT_WALK_SPEC 0            // 1: leaves parked and tested together (speculative traversal)
-#endif
-#ifndef RT_BVH_WHILE_WHILE
-#define RT_BVH_WHILE_WHILE 0
-#endif
-
-#ifndef RT_BVH_UNIFORM
-#define RT_BVH_UNIFORM 1
-#endif
-
-// Both children of a two-child node: (lo - olo) * inv as fma(lo, inv, -olo * inv) for the pair of
-// children at once (same rounding as bvh_box_hit's FMA form).
-#ifndef RT_BVH_PACKED
-#define RT_BVH_PACKED 1           // 0: twelve scalar FMAs (no duplicated {inv, inv} register pairs)
-#endif
-#ifndef RT_BVH_MINIMUM
-#define RT_BVH_MINIMUM 1
-#endif
-#if RT_BVH_MINIMUM && defined(__HIP_DEVICE_COMPILE__)
 // IEEE 754-2019 minimum / maximum (v_minimum3_f32 / v_maximum3_f32 on gfx950): unlike fminf / fmaxf
 // they need no canonicalized inputs, so the loop-carried ray limit is not re-canonicalized at every
 // node.  They differ from fminf / fmaxf only for NaN operands (propagated instead of dropped: a NaN
@@ -528,19 +412,17 @@ typedef float rt_f2 __attribute__((ext_vector_type(2)));
 #define RT_SLAB_MIN(a, b) fminf(a, b)
 #define RT_SLAB_MAX(a, b) fmaxf(a, b)
 #endif
+
+// Both children of a two-child node: (lo - olo) * inv as fma(lo, inv, -olo * inv), the pair of
+// children at once as packed FMAs (v_pk_fma_f32): 6 per node.
 RT_HD void bvh_node2_hit(const Bvh2Node& n, const BvhRay& r, float tlimit, bool& h0, bool& h1, float& t0,
                          float& t1) {
     rt_f2 a[3], b[3];
     for (int k = 0; k < 3; ++k) {
-#if RT_BVH_PACKED
         const rt_f2 inv = {r.inv[k], r.inv[k]};
         const rt_f2 slo = {-r.slo[k], -r.slo[k]}, shi = {-r.shi[k], -r.shi[k]};
         a[k] = __builtin_elementwise_fma(rt_f2{n.lo[k][0], n.lo[k][1]}, inv, slo);
         b[k] = __builtin_elementwise_fma(rt_f2{n.hi[k][0], n.hi[k][1]}, inv, shi);
-#else
-        a[k] = rt_f2{__builtin_fmaf(n.lo[k][0], r.inv[k], -r.slo[k]), __builtin_fmaf(n.lo[k][1], r.inv[k], -r.slo[k])};
-        b[k] = rt_f2{__builtin_fmaf(n.hi[k][0], r.inv[k], -r.shi[k]), __builtin_fmaf(n.hi[k][1], r.inv[k], -r.shi[k])};
-#endif
     }
 #define MN RT_SLAB_MIN
 #define MX RT_SLAB_MAX
@@ -554,186 +436,51 @@ RT_HD void bvh_node2_hit(const Bvh2Node& n, const BvhRay& r, float tlimit, bool&
     h1 = t1 <= f1;
 }
 
-// Half-precision node: the binary16 bounds widen exactly to binary32 inside the FMA (v_fma_mix_f32).
-RT_HD void bvh_node2_hit(const Bvh2NodeH& n, const BvhRay& r, float tlimit, bool& h0, bool& h1, float& t0,
-                         float& t1) {
-    // both 16-B halves of the node in flight at once (the compiler otherwise waits for the first
-    // before issuing the second: two memory round trips per node)
-    uint32_t q[6];
-    memcpy(q, &n, sizeof q);
-    for (int i = 0; i < 6; ++i) RT_KEEP(q[i]);
-    auto lo = [&](int k, int c) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(q[k] >> (16 * c))); };
-    auto hi = [&](int k, int c) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(q[3 + k] >> (16 * c))); };
-    float a[3][2], b[3][2];
-    for (int k = 0; k < 3; ++k)
-        for (int c = 0; c < 2; ++c) {
-            a[k][c] = __builtin_fmaf(lo(k, c), r.inv[k], -r.slo[k]);
-            b[k][c] = __builtin_fmaf(hi(k, c), r.inv[k], -r.shi[k]);
-        }
-    t0 = fmaxf(fmaxf(fminf(a[0][0], b[0][0]), fminf(a[1][0], b[1][0])), fmaxf(fminf(a[2][0], b[2][0]), 0.0f));
-    t1 = fmaxf(fmaxf(fminf(a[0][1], b[0][1]), fminf(a[1][1], b[1][1])), fmaxf(fminf(a[2][1], b[2][1]), 0.0f));
-    const float f0 = fminf(fminf(fmaxf(a[0][0], b[0][0]), fmaxf(a[1][0], b[1][0])), fminf(fmaxf(a[2][0], b[2][0]), tlimit));
-    const float f1 = fminf(fminf(fmaxf(a[0][1], b[0][1]), fmaxf(a[1][1], b[1][1])), fminf(fmaxf(a[2][1], b[2][1]), tlimit));
-    h0 = t0 <= f0;
-    h1 = t1 <= f1;
-}
-
-#ifndef RT_BVH_BUFFER
-#define RT_BVH_BUFFER 1           // per-lane node reads as buffer loads (32-bit offsets): RTOW +1.4 %, f32 +2 %
-#endif
-#ifndef RT_LEAF_BUFFER
-#define RT_LEAF_BUFFER 0          // 1: leaf records read as buffer loads too
-#endif
-#if (RT_BVH_BUFFER || RT_LEAF_BUFFER) && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
 typedef unsigned int rt_u4 __attribute__((ext_vector_type(4)));
-// record i of a 16-B-multiple array behind a raw buffer descriptor (32-bit offset, no 64-bit address math)
-template <class T>
-__device__ __forceinline__ T load_rec(__amdgpu_buffer_rsrc_t rs, int i) {
-    static_assert(sizeof(T) % 16 == 0, "16-B records");
-    const int off = i * (int)sizeof(T);
-    rt_u4 q[sizeof(T) / 16];
-    for (int k = 0; k < (int)(sizeof(T) / 16); ++k) q[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * k, 0, 0);
-    T n;
+// node i behind a raw buffer descriptor: 32-bit offsets, no 64-bit address arithmetic per node
+// (RTOW +1.4 %, f32 +2 %)
+__device__ __forceinline__ Bvh2Node load_node(__amdgpu_buffer_rsrc_t rs, int i) {
+    const int off = i * (int)sizeof(Bvh2Node);
+    rt_u4 q[sizeof(Bvh2Node) / 16];
+    for (int k = 0; k < (int)(sizeof(Bvh2Node) / 16); ++k) q[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * k, 0, 0);
+    Bvh2Node n;
     memcpy(&n, q, sizeof n);
     return n;
 }
-__device__ __forceinline__ WideNode load_wide(__amdgpu_buffer_rsrc_t rs, int i) { return load_rec<WideNode>(rs, i); }
 #endif
 
 // Walk one BVH and call leaf(fc) for every leaf whose box the ray reaches before the current best.
 // WIDE: ordered walk over Bvh2Node (both child boxes per 64-B node, nearer child first, the other
-// pushed on the lane's stack); otherwise the stackless preorder walk over BvhNode skip links.
+// pushed on the lane's stack); otherwise the stackless preorder walk over BvhNode skip links (A/B and
+// host cross-check).  Variants measured slower and removed: postponed leaves,
+// "while-while" leaf batching, binary16 child boxes, four-child nodes, stack top in a register, leaf
+// records as buffer loads.
 template <bool WIDE, class Leaf>
-RT_HD void bvh_walk(const BvhNode* nodes, int count, const WideNode* wide, const BvhRay& br, const float& tl,
+RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const BvhRay& br, const float& tl,
                     BvhStack stk, Work& w, Leaf&& leaf) {
     if constexpr (WIDE) {
-#if RT_BVH_WHILE_WHILE
-        // "while-while": descend inner nodes until this lane holds a leaf (or its walk is over), then
-        // test the leaf; the wave runs the (binary64) leaf code once for all lanes holding one
-        // instead of in every inner-node iteration
         int sp = 0, cur = 0;
-        bool live = true;
-        while (live) {
-            while (cur >= 0) {
-                const WideNode n = wide[cur];
-                RT_COUNT(++w.nodes);
-                float t0, t1;
-                bool h0, h1;
-                bvh_node2_hit(n, br, tl, h0, h1, t0, t1);
-                if (h0 && h1) {
-                    const bool swap = t1 < t0;
-                    stk.base[(sp++) * stk.stride] = swap ? n.child[0] : n.child[1];
-                    cur = swap ? n.child[1] : n.child[0];
-                } else if (h0 | h1) {
-                    cur = h0 ? n.child[0] : n.child[1];
-                } else if (sp > 0) {
-                    cur = stk.base[(--sp) * stk.stride];
-                } else {
-                    live = false;
-                    break;
-                }
-            }
-            if (!live) break;
-            leaf(~cur);
-            if (sp == 0) break;
-            cur = stk.base[(--sp) * stk.stride];
-        }
-#else
-        int sp = 0, cur = 0;
-#if RT_BVH_BUFFER && RT_BVH_UNIFORM && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
         const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)wide, (short)0, 0x7FFFFFFF, 0x00020000);
 #endif
-#if RT_STACK_TOP
-        int top = RT_CHILD_EMPTY;   // never a node or leaf reference (leaves hold <= 15 primitives)
-#endif
-        auto push = [&](int c) {
-#if RT_STACK_TOP
-            if (top != RT_CHILD_EMPTY) stk.base[(sp++) * stk.stride] = top;
-            top = c;
-#else
-            stk.base[(sp++) * stk.stride] = c;
-#endif
-        };
-        auto pop = [&]() -> bool {    // false: the walk is over
-#if RT_STACK_TOP
-            if (top != RT_CHILD_EMPTY) {
-                cur = top;
-                top = RT_CHILD_EMPTY;
-                return true;
-            }
-#endif
-            if (sp == 0) return false;
-            cur = stk.base[(--sp) * stk.stride];
-            return true;
-        };
         // true: descend to the new cur
-        auto step = [&](const WideNode& n) -> bool {
+        auto step = [&](const Bvh2Node& n) -> bool {
             float t0, t1;
             bool h0, h1;
             bvh_node2_hit(n, br, tl, h0, h1, t0, t1);
-#if RT_NODE_PREFETCH
             // branch-free child selection: the child indices are consumed by selects ahead of any
             // branch, so their loads issue with the box loads (no dependent round trip after the
-            // slab test)
+            // slab test).  Near child = child 1 iff h1 and (!h0 or t1 < t0), written as plain mask
+            // logic: the compiler keeps it in SGPR masks (3 scalar ops) instead of materializing
+            // booleans in VGPRs (7 vector ops per node; RTOW +2.7 %)
             const int c0 = n.child[0], c1 = n.child[1];
-            const bool both = h0 && h1;
-            // near child = child 1 iff h1 and (!h0 or t1 < t0), written as plain mask logic: the
-            // compiler keeps it in SGPR masks (3 scalar ops) instead of materializing booleans in
-            // VGPRs (7 vector ops per node; RTOW +2.7 %)
             const bool take1 = h1 & (!h0 | (t1 < t0));
             const int near_c = take1 ? c1 : c0, far_c = take1 ? c0 : c1;
-            if (both) push(far_c);
+            if (h0 && h1) stk.base[(sp++) * stk.stride] = far_c;
             cur = (h0 | h1) ? near_c : cur;
             return h0 | h1;
-#else
-            if (h0 && h1) {
-                const bool swap = t1 < t0;
-                push(swap ? n.child[0] : n.child[1]);
-                cur = swap ? n.child[1] : n.child[0];
-                return true;
-            }
-            if (h0 | h1) {
-                cur = h0 ? n.child[0] : n.child[1];
-                return true;
-            }
-            return false;
-#endif
         };
-#if RT_WALK_SPEC && defined(__HIP_DEVICE_COMPILE__)
-        // Postponed leaves (speculative traversal): a lane that reaches a leaf parks it in `pend` and
-        // goes on walking inner nodes; the parked leaves are tested together once no lane of the
-        // wave is still looking for one (a lane that reaches a second leaf waits for that).  The
-        // closest hit does not depend on the visiting order (comment above `better`); a stale tl only
-        // visits more nodes, never fewer, so the result is bit-identical.
-        int pend = 0;                  // parked leaf reference (< 0), 0 = none
-        bool walking = true;
-        for (;;) {
-#if RT_PROFILE
-            ++w.lane_trips;
-            if ((int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) ++w.wave_trips;
-#endif
-            if (walking) {
-                if (cur >= 0) {
-                    RT_COUNT(++w.nodes);
-#if RT_BVH_UNIFORM
-                    const int first = __builtin_amdgcn_readfirstlane(cur);
-                    const bool down = __ballot(cur != first) == 0 ? step(wide[first]) : step(wide[cur]);
-#else
-                    const bool down = step(wide[cur]);
-#endif
-                    if (!down && !pop()) walking = false;
-                } else if (pend == 0) {
-                    pend = cur;
-                    if (!pop()) walking = false;
-                }
-            }
-            if (__ballot(walking && pend == 0) == 0 && pend != 0) {   // no lane still looking for a leaf
-                leaf(~pend);
-                pend = 0;
-            }
-            if (!walking && pend == 0) break;
-        }
-#else
         for (;;) {
 #if RT_PROFILE && defined(__HIP_DEVICE_COMPILE__)
             ++w.lane_trips;                       // the first active lane counts the wave's iteration
@@ -747,28 +494,21 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const WideNode* wide, const
             bool down = false;
             if (cur >= 0) {
                 RT_COUNT(++w.nodes);
-#if RT_BVH_UNIFORM && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
                 // every active lane at the same node (30 % of RTOW walk steps, 49 % on mesh50k): read
-                // it with scalar loads, which bypass the vector memory pipeline
+                // it with scalar loads, which bypass the vector memory pipeline (+3.5 %)
                 const int first = __builtin_amdgcn_readfirstlane(cur);
-#if RT_BVH_BUFFER
-                down = __ballot(cur != first) == 0 ? step(wide[first]) : step(load_wide(wrs, cur));
-#else
-                down = __ballot(cur != first) == 0 ? step(wide[first]) : step(wide[cur]);
-#endif
+                down = __ballot(cur != first) == 0 ? step(wide[first]) : step(load_node(wrs, cur));
 #else
                 down = step(wide[cur]);
 #endif
-#if !RT_WALK_IFIF
                 if (down) continue;
-#endif
             } else {
                 leaf(~cur);      // (scalar leaf reads for wave-uniform leaves measured 2 % slower)
             }
-            if (!down && !pop()) break;
+            if (sp == 0) break;
+            cur = stk.base[(--sp) * stk.stride];
         }
-#endif  // RT_WALK_SPEC
-#endif
     } else {
         int ni = 0;
         while (ni < count) {
@@ -782,9 +522,6 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const WideNode* wide, const
     }
 }
 
-// Closest hit through the BVHs: planes and boxes (usually few, often large) brute force first, then
-// the sphere BVH and the triangle BVH.  Lanes walk their own paths (per-lane node loads); leaf
-// records are contiguous in leaf order.
 // Planes and boxes (usually few, often large) brute force, with their World.objects index.
 template <class R>
 RT_HD void brute_planes_boxes(const SceneView<R>& sc, V3<R> o, V3<R> d, R tmin, Closest<R>& b) {
@@ -824,37 +561,12 @@ RT_HD void sphere_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R a, co
                        Closest<R>& b, float& tl, Work& w) {
     const int first = fc >> 4, end = first + (fc & 15);
     RT_COUNT(w.spheres += end - first);
-#if RT_LEAF_BUFFER && defined(__HIP_DEVICE_COMPILE__)
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)sc.bvh_sphere_leaf, (short)0, 0x7FFFFFFF, 0x00020000);
-#endif
     for (int k = first; k < end; ++k) {
-#if RT_LEAF_BUFFER && defined(__HIP_DEVICE_COMPILE__)
-        SphereLeaf<R> L = load_rec<SphereLeaf<R>>(rs, k);
-#else
-        SphereLeaf<R> L = sc.bvh_sphere_leaf[k];
-#endif
-#if RT_LEAF_PREFETCH
-        RT_KEEP(L.s.cx); RT_KEEP(L.s.cy); RT_KEEP(L.s.cz); RT_KEEP(L.s.r2);
-        RT_KEEP(L.id); RT_KEEP(L.obj); RT_KEEP(L.mat);
-#endif
+        const SphereLeaf<R> L = sc.bvh_sphere_leaf[k];
         if constexpr (sizeof(R) == 8)
             if (!sphere_filter_pass(L.f, fr)) continue;
-#if RT_WORK_EXTRA
-        {   // x0: binary64 tests, x1: of those moving away from an outside centre (hb > 0, c >= 0),
-            // x2: candidates (t >= tmin), x3: accepted as the new best
-            ++w.x[0];
-            const R ocx = o.x - L.s.cx, ocy = o.y - L.s.cy, ocz = o.z - L.s.cz;
-            const R hb = ocx * d.x + ocy * d.y + ocz * d.z;
-            const R c = (ocx * ocx + ocy * ocy + ocz * ocz) - L.s.r2;
-            if (hb > (R)0 && c >= (R)0) ++w.x[1];
-        }
-#endif
         R t;
         if (!sphere_candidate(L.s, o, d, a, tmin, t)) continue;
-#if RT_WORK_EXTRA
-        ++w.x[2];
-        if (better(t, L.obj, L.id, b)) ++w.x[3];
-#endif
         if (better(t, L.obj, L.id, b)) {
             b = Closest<R>{t, HIT_SPHERE, L.id, L.mat, L.obj};
             tl = bvh_tlimit(b.t);
@@ -866,19 +578,8 @@ template <class R>
 RT_HD void tri_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R tmin, Closest<R>& b, float& tl, Work& w) {
     const int first = fc >> 4, end = first + (fc & 15);
     RT_COUNT(w.tris += end - first);
-#if RT_LEAF_BUFFER && defined(__HIP_DEVICE_COMPILE__)
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)sc.bvh_tri_leaf, (short)0, 0x7FFFFFFF, 0x00020000);
-#endif
     for (int k = first; k < end; ++k) {
-#if RT_LEAF_BUFFER && defined(__HIP_DEVICE_COMPILE__)
-        TriLeaf<R> L = load_rec<TriLeaf<R>>(rs, k);
-#else
-        TriLeaf<R> L = sc.bvh_tri_leaf[k];
-#endif
-#if RT_LEAF_PREFETCH
-        RT_KEEP(L.t.v0x); RT_KEEP(L.t.e1x); RT_KEEP(L.t.e2x); RT_KEEP(L.t.nz);
-        RT_KEEP(L.id); RT_KEEP(L.obj); RT_KEEP(L.mat);
-#endif
+        const TriLeaf<R> L = sc.bvh_tri_leaf[k];
         R t;
         if (!triangle_candidate(L.t, o, d, tmin, t)) continue;
         if (better(t, L.obj, L.id, b)) {
@@ -890,73 +591,9 @@ RT_HD void tri_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R tmin, Cl
 
 // Closest hit through the BVHs: planes and boxes brute force first (their t shortens the walks),
 // then the sphere BVH and the triangle BVH.  Lanes walk their own paths (per-lane node loads); leaf
-// records are contiguous in leaf order.
-// Four children at once: entry distance and hit flag per child (pairs (0,1), (2,3) as packed FMAs).
-RT_HD void bvh_node4_hit(const Bvh4Node& n, const BvhRay& r, float tlimit, float tn[4], bool hit[4]) {
-    for (int p = 0; p < 4; p += 2) {
-        rt_f2 a[3], b[3];
-        for (int k = 0; k < 3; ++k) {
-            const rt_f2 inv = {r.inv[k], r.inv[k]};
-            const rt_f2 slo = {-r.slo[k], -r.slo[k]}, shi = {-r.shi[k], -r.shi[k]};
-            a[k] = __builtin_elementwise_fma(rt_f2{n.lo[k][p], n.lo[k][p + 1]}, inv, slo);
-            b[k] = __builtin_elementwise_fma(rt_f2{n.hi[k][p], n.hi[k][p + 1]}, inv, shi);
-        }
-        tn[p] = fmaxf(fmaxf(fminf(a[0].x, b[0].x), fminf(a[1].x, b[1].x)), fmaxf(fminf(a[2].x, b[2].x), 0.0f));
-        tn[p + 1] = fmaxf(fmaxf(fminf(a[0].y, b[0].y), fminf(a[1].y, b[1].y)), fmaxf(fminf(a[2].y, b[2].y), 0.0f));
-        const float f0 = fminf(fminf(fmaxf(a[0].x, b[0].x), fmaxf(a[1].x, b[1].x)), fminf(fmaxf(a[2].x, b[2].x), tlimit));
-        const float f1 = fminf(fminf(fmaxf(a[0].y, b[0].y), fmaxf(a[1].y, b[1].y)), fminf(fmaxf(a[2].y, b[2].y), tlimit));
-        hit[p] = tn[p] <= f0 && n.child[p] != RT_CHILD_EMPTY;
-        hit[p + 1] = tn[p + 1] <= f1 && n.child[p + 1] != RT_CHILD_EMPTY;
-    }
-}
-
-// Ordered walk over four-child nodes: the hit children sorted by entry distance (a 5-exchange
-// network on (distance, child) with misses as (+inf, EMPTY)), the nearest taken, the others pushed
-// farthest first.  Every hit child is visited (a child whose f32 entry distance overflowed to +inf
-// sorts among the misses but keeps its reference), so culling stays exactly that of the slab test.
-template <class Leaf>
-RT_HD void bvh_walk4(const Bvh4Node* nodes, const BvhRay& br, const float& tl, BvhStack stk, Work& w, Leaf&& leaf) {
-    int sp = 0, cur = 0;
-    for (;;) {
-        if (cur >= 0) {
-            const Bvh4Node n = nodes[cur];
-            RT_COUNT(++w.nodes);
-            float key[4];
-            bool hit[4];
-            bvh_node4_hit(n, br, tl, key, hit);
-            int c[4];
-            for (int k = 0; k < 4; ++k) {
-                c[k] = hit[k] ? n.child[k] : RT_CHILD_EMPTY;
-                key[k] = hit[k] ? key[k] : INFINITY;
-            }
-            auto cx = [&](int i, int j) {
-                if (key[j] < key[i]) {
-                    const float tk = key[i]; key[i] = key[j]; key[j] = tk;
-                    const int tc = c[i]; c[i] = c[j]; c[j] = tc;
-                }
-            };
-#if RT_BVH4_SORT
-            cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
-#else
-            cx(0, 1); cx(2, 3); cx(0, 2);          // nearest first; the rest pushed unordered
-#endif
-            for (int k = 3; k >= 1; --k)
-                if (c[k] != RT_CHILD_EMPTY) stk.base[(sp++) * stk.stride] = c[k];
-            if (c[0] != RT_CHILD_EMPTY) {
-                cur = c[0];
-                continue;
-            }
-        } else {
-            leaf(~cur);
-        }
-        if (sp == 0) break;
-        cur = stk.base[(--sp) * stk.stride];
-    }
-}
-
-// WALK: 0 = stackless preorder (BvhNode), 1 = ordered two-child (Bvh2Node), 2 = ordered four-child
-// (Bvh4Node)
-template <class R, int WALK>
+// records are contiguous in leaf order.  WIDE: the ordered two-child walk (default); else the
+// stackless preorder walk.
+template <class R, bool WIDE>
 RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
     const R tmin = (R)0.001;
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
@@ -968,27 +605,23 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
         FilterRay fr{};
         if constexpr (sizeof(R) == 8) fr = make_filter_ray(o, d);
         auto leaf = [&](int fc) { sphere_leaf(sc, fc, o, d, a, fr, tmin, b, tl, w); };
-        if constexpr (WALK == 2) bvh_walk4(sc.sphere_wide4, br, tl, stk, w, leaf);
-        else bvh_walk<WALK == 1>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w, leaf);
+        bvh_walk<WIDE>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w, leaf);
     }
     if (sc.num_tri_nodes > 0) {
         auto leaf = [&](int fc) { tri_leaf(sc, fc, o, d, tmin, b, tl, w); };
-        if constexpr (WALK == 2) bvh_walk4(sc.tri_wide4, br, tl, stk, w, leaf);
-        else bvh_walk<WALK == 1>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, leaf);
+        bvh_walk<WIDE>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, leaf);
     }
     return b;
 }
 
 // acceleration modes of the trace kernel
-enum Accel : int { ACC_BRUTE = 0, ACC_LDS = 1, ACC_BVH = 2, ACC_BVH_STACK = 3, ACC_BVH4 = 4 };
+enum Accel : int { ACC_BRUTE = 0, ACC_BVH = 2, ACC_BVH_STACK = 3 };
 
 template <class R, int ACC>
-RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, const LdsSpheres lds, Work& w,
-                                 BvhStack stk) {
-    if constexpr (ACC == ACC_BVH) return closest_hit_bvh<R, 0>(sc, o, d, w, stk);
-    else if constexpr (ACC == ACC_BVH_STACK) return closest_hit_bvh<R, 1>(sc, o, d, w, stk);
-    else if constexpr (ACC == ACC_BVH4) return closest_hit_bvh<R, 2>(sc, o, d, w, stk);
-    else return closest_hit<R, ACC == ACC_LDS>(sc, o, d, lds);
+RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
+    if constexpr (ACC == ACC_BVH) return closest_hit_bvh<R, false>(sc, o, d, w, stk);
+    else if constexpr (ACC == ACC_BVH_STACK) return closest_hit_bvh<R, true>(sc, o, d, w, stk);
+    else return closest_hit<R>(sc, o, d);
 }
 
 template <class R>

@@ -9,32 +9,32 @@ namespace rt {
 
 // Counters::totals slots: 0 segments, 1 BVH nodes, 2 sphere tests, 3 triangle tests; RT_PROFILE builds:
 // 4..6 cycles (closest hit, shading, regeneration), 7 / 8 walk iterations per lane / per wave, 9 wave
-// iterations whose active lanes all sit at one inner node; slot kQueueSlot: the pixel-queue head
+// iterations whose active lanes all sit at one inner node
 constexpr int kTotalSlots = 12;
-constexpr int kQueueSlot = 11;
+
+// chunk partial sums of one 8x8 tile: 3 channels x 64 pixels, binary64
+constexpr size_t kPartialBytesPerTile = 3 * 64 * sizeof(double);
 
 struct Counters {
     double* sum;               // n*3 running per-pixel radiance sums (read-modify-write)
     uint32_t* segs;            // optional n per-pixel world.hit counts
     uint32_t* draws;           // optional n per-pixel RNG draws
     unsigned long long* totals;   // optional [segments, BVH nodes, sphere tests, triangle tests]
-    unsigned long long* queue = nullptr;   // pixel-queue head (RT_PIXEL_QUEUE builds), zeroed per launch
-    void* pool = nullptr;      // sample-pool radiance buffer (trace_uses_pool()): per-sample radiance
-    size_t pool_bytes = 0;     // of up to pool_bytes / pool_sample_bytes(cw, ch, sizeof(R)) samples per launch
+    double* part = nullptr;    // sample-pool chunk partials (scratch, pool_partial_bytes)
+    size_t part_bytes = 0;
 };
 
+// bvh: walk the BVHs (ACC_BVH_STACK, the ordered two-child walk), else World order (ACC_BRUTE)
 template <class R>
-// walk: ACC_BRUTE (World order), ACC_BVH_STACK (two-child BVH walk) or ACC_BVH4 (four-child walk)
-hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, int walk, hipStream_t stream);
+hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh, hipStream_t stream);
 
-// true: launch_trace runs the sample-pool kernel, which needs Counters::pool (at least one sample of
-// the crop: pool_sample_bytes); RT_SAMPLE_POOL=0 in the environment selects the lane-per-pixel
-// kernel (A/B runs, tests)
+// true: launch_trace runs the sample-pool kernel; RT_SAMPLE_POOL=0 in the environment selects the
+// lane-per-pixel kernel (A/B runs, tests)
 bool trace_uses_pool();
-// bytes the pool holds per sample of a cw x ch crop: 64 pixels per 8x8 tile (edge tiles padded)
-inline size_t pool_sample_bytes(int cw, int ch, size_t real_bytes) {
-    return (size_t)((cw + 7) / 8) * (size_t)((ch + 7) / 8) * 64 * 3 * real_bytes;
-}
+// scratch bytes the sample pool needs to trace `ns` samples of a cw x ch crop in one launch (0: one
+// chunk, the partials go straight to the sums).  With less scratch (but at least one chunk's worth,
+// tiles x kPartialBytesPerTile) launch_trace splits the samples over several launches.
+size_t pool_partial_bytes(int cw, int ch, int ns, bool tri_bvh);
 
 struct FinalizeParams {
     int n;

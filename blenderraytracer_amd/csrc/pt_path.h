@@ -70,26 +70,20 @@ RT_HD void start_sample(const SceneView<R>& sc, const ImageParams& im, int i, in
 }
 
 // x^5 for Schlick's approximation (materials.js:79-83, Math.pow(1 - cosine, 5)), correctly rounded.
-// V8's Math.pow (fdlibm) and glibc's pow return the correctly rounded x^5 for these arguments; the
-// device pow (ocml, <= 1 ulp) costs ~100 binary64 instructions and is not always correctly rounded.
-// Here x^2, x^4, x^5 are carried as unevaluated sums hi + lo (error-free products by FMA): the pair
-// approximates x^5 to ~2^-100 relative, so the single final rounding gives RN(x^5) unless x^5 lies
-// within 2^-100 of a rounding midpoint.  10 binary64 ops; exact for x = 0 and x = 1.  Checked against
-// libm pow bit for bit (tests/test_hostcheck.py::test_pow5_correctly_rounded).  RT_POW5 = 0: device pow
-// (A/B).  Only for 0 <= x <= 2 (no overflow/underflow concerns: x is 0 or >= 2^-53).
-#ifndef RT_POW5
-#define RT_POW5 1
-#endif
+// Neither V8's Math.pow (fdlibm) nor glibc's pow is always correctly rounded (both <= ~0.5 ulp), and
+// the device pow (ocml, <= 1 ulp) costs ~100 binary64 instructions.  Here x^2, x^4, x^5 are carried
+// as unevaluated sums hi + lo (error-free products by FMA): the pair approximates x^5 to ~2^-100
+// relative, so the single final rounding gives RN(x^5) unless x^5 lies within 2^-100 of a rounding
+// midpoint.  10 binary64 ops; exact for x = 0 and x = 1.  Checked against exact rationals
+// (tests/test_hostcheck.py::test_pow5_correctly_rounded) and against Node's own Math.pow(x, 5) on the
+// same arguments (tests/test_js_host.py::test_pow5_vs_v8_math_pow, which reports the mismatch rate).
+// Only for 0 <= x <= 2 (no overflow/underflow concerns: x is 0 or >= 2^-53).
 template <class R>
 RT_HD R pow5_rn(R x) {
-#if RT_POW5
     const R p = x * x, pe = fma(x, x, -p);                 // x^2 = p + pe exactly
     const R q = p * p, qe = fma(p, p, -q) + (R)2 * (p * pe); // x^4 ~ q + qe
     const R r = q * x, re = fma(q, x, -r) + qe * x;          // x^5 ~ r + re
     return r + re;
-#else
-    return pow(x, (R)5);
-#endif
 }
 
 // Scatter at a non-emissive hit (materials.js:20-83).  Returns false when Metal absorbs.
@@ -174,7 +168,7 @@ RT_HD bool shade_segment(const SceneView<R>& sc, const Closest<R>& c, V3<R>& o, 
 // Trace samples [im.s_begin, s_end) of crop pixel (cx, cy), adding radiance into sum[0..2].
 template <class R, bool COUNT, int ACC = ACC_BRUTE>
 RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int cx, int cy, int s_end, double* sum,
-                              const LdsSpheres lds = LdsSpheres{nullptr}, BvhStack stk = BvhStack{nullptr, 0}) {
+                              BvhStack stk = BvhStack{nullptr, 0}) {
     const int i = im.x0 + cx, row = im.y0 + cy, j = im.height - 1 - row;
     const uint32_t pkey = pixel_key(im.seedm, (uint32_t)row * (uint32_t)im.width + (uint32_t)i);
     PixelResult res{0, 0, {0, 0, 0}, {0, 0, 0}};
@@ -186,7 +180,7 @@ RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int
     if (s < s_end) start_sample(sc, im, i, j, pkey, s, g, o, d);
     while (s < s_end) {
         const uint64_t t0 = RT_TICK();
-        const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, lds, res.work, stk);
+        const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, res.work, stk);
         const uint64_t t1 = RT_TICK();
         if (RT_PROFILE) res.cyc[0] += t1 - t0;
         ++res.segments;
@@ -205,88 +199,6 @@ RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int
         if (RT_PROFILE) res.cyc[2] += RT_TICK() - t2;
     }
     sum[0] = sx; sum[1] = sy; sum[2] = sz;
-    return res;
-}
-
-// Pixel-queue order: 8x8 blocks of the crop in raster order, the 64 pixels of a block consecutive, so
-// a wave's first fetch takes one whole block.  Positions past the crop's right/bottom edge are skipped.
-RT_HD uint32_t queue_length(const ImageParams& im) {
-    return (uint32_t)((im.cw + 7) / 8) * (uint32_t)((im.ch + 7) / 8) * 64u;
-}
-RT_HD bool queue_pixel(const ImageParams& im, uint32_t p, int& cx, int& cy) {
-    const uint32_t tiles_x = (uint32_t)(im.cw + 7) / 8, t = p >> 6, w = p & 63;
-    cx = (int)((t % tiles_x) * 8 + (w & 7));
-    cy = (int)((t / tiles_x) * 8 + (w >> 3));
-    return cx < im.cw && cy < im.ch;
-}
-
-// Pixel-queue variant of trace_pixel: a lane whose pixel has finished its samples takes the next
-// pixel index from `fetch()` (a wave-aggregated atomic on the GPU) inside the same loop, so no lane
-// idles while another pixel of its wave is still tracing.  Each pixel's samples and results are
-// exactly trace_pixel's (same keys, same order); sum/segs/draws are indexed by crop pixel.
-template <class R, bool COUNT, int ACC, class Fetch>
-RT_HD PixelResult trace_pixels_queue(const SceneView<R>& sc, const ImageParams& im, Fetch&& fetch, double* sum,
-                                     uint32_t* segs, uint32_t* draws, const LdsSpheres lds, BvhStack stk) {
-    PixelResult res{0, 0, {0, 0, 0}, {0, 0, 0}};
-    const uint32_t n = queue_length(im);
-    Rng<R> g;
-    V3<R> o, d, T = mk<R>(1, 1, 1);
-    int depth = im.max_depth, i = 0, j = 0, s = 0;
-    uint32_t pkey = 0, psegs = 0, pdraws = 0;
-    size_t q = 0;
-    double sx = 0, sy = 0, sz = 0;
-    auto next_pixel = [&]() -> bool {
-        for (;;) {
-            const uint32_t p = fetch();
-            if (p >= n) return false;
-            int cx, cy;
-            if (!queue_pixel(im, p, cx, cy)) continue;
-            const int row = im.y0 + cy;
-            i = im.x0 + cx;
-            j = im.height - 1 - row;
-            pkey = pixel_key(im.seedm, (uint32_t)row * (uint32_t)im.width + (uint32_t)i);
-            q = (size_t)cy * im.cw + cx;
-            sx = sum[3 * q]; sy = sum[3 * q + 1]; sz = sum[3 * q + 2];
-            psegs = pdraws = 0;
-            s = im.s_begin;
-            T = mk<R>(1, 1, 1);
-            depth = im.max_depth;
-            start_sample(sc, im, i, j, pkey, s, g, o, d);
-            return true;
-        }
-    };
-    bool live = im.s_begin < im.s_end && next_pixel();
-    while (live) {
-        const uint64_t t0 = RT_TICK();
-        const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, lds, res.work, stk);
-        const uint64_t t1 = RT_TICK();
-        if (RT_PROFILE) res.cyc[0] += t1 - t0;
-        ++psegs;
-        V3<R> L;
-        const bool done = shade_segment(sc, c, o, d, T, depth, g, L);
-        const uint64_t t2 = RT_TICK();
-        if (RT_PROFILE) res.cyc[1] += t2 - t1;
-        if (done) {
-            sx += (double)L.x; sy += (double)L.y; sz += (double)L.z;
-            if (COUNT) pdraws += g.k;
-            ++s;
-            T = mk<R>(1, 1, 1);
-            depth = im.max_depth;
-            if (s < im.s_end) {
-                start_sample(sc, im, i, j, pkey, s, g, o, d);
-            } else {
-                sum[3 * q] = sx; sum[3 * q + 1] = sy; sum[3 * q + 2] = sz;
-                if (COUNT) {
-                    if (segs) segs[q] += psegs;
-                    if (draws) draws[q] += pdraws;
-                }
-                res.segments += psegs;
-                res.draws += pdraws;
-                live = next_pixel();
-            }
-        }
-        if (RT_PROFILE) res.cyc[2] += RT_TICK() - t2;
-    }
     return res;
 }
 

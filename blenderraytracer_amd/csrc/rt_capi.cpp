@@ -98,15 +98,14 @@ struct DeviceScene {
     DevBuf<BvhNode> sphere_nodes, tri_nodes;
     DevBuf<SphereLeaf<R>> bvh_sphere_leaf;
     DevBuf<TriLeaf<R>> bvh_tri_leaf;
-    DevBuf<WideNode> sphere_wide, tri_wide;
-    DevBuf<Bvh4Node> sphere_wide4, tri_wide4;
+    DevBuf<Bvh2Node> sphere_wide, tri_wide;
     SceneView<R> view{};
     void release() {
         runs.release(); spheres.release(); sphere_filter.release(); sphere_r.release(); planes.release(); boxes.release(); tris.release();
         sphere_mat.release(); plane_mat.release(); box_mat.release(); tri_mat.release(); perm.release(); mats.release();
         plane_obj.release(); box_obj.release(); sphere_nodes.release(); tri_nodes.release(); bvh_sphere_leaf.release();
         bvh_tri_leaf.release();
-        sphere_wide.release(); tri_wide.release(); sphere_wide4.release(); tri_wide4.release();
+        sphere_wide.release(); tri_wide.release();
     }
 };
 
@@ -121,7 +120,6 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     UP(box_mat, hs.box_mat); UP(tri_mat, hs.tri_mat); UP(perm, rec.perm); UP(mats, rec.mats);
     UP(plane_obj, hs.plane_obj); UP(box_obj, hs.box_obj); UP(sphere_nodes, hs.sphere_bvh); UP(tri_nodes, hs.tri_bvh);
     UP(bvh_sphere_leaf, rec.bvh_sphere_leaf); UP(bvh_tri_leaf, rec.bvh_tri_leaf); UP(sphere_wide, hs.sphere_wide); UP(tri_wide, hs.tri_wide);
-    UP(sphere_wide4, hs.sphere_wide4); UP(tri_wide4, hs.tri_wide4);
 #undef UP
     if (e != hipSuccess) return fail(RT_ERR_DEVICE, "scene upload: %s", hipGetErrorString(e));
     SceneView<R>& v = ds.view;
@@ -132,7 +130,6 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     v.plane_obj = ds.plane_obj.p; v.box_obj = ds.box_obj.p; v.sphere_nodes = ds.sphere_nodes.p; v.tri_nodes = ds.tri_nodes.p;
     v.bvh_sphere_leaf = ds.bvh_sphere_leaf.p; v.bvh_tri_leaf = ds.bvh_tri_leaf.p;
     v.sphere_wide = ds.sphere_wide.p; v.tri_wide = ds.tri_wide.p;
-    v.sphere_wide4 = ds.sphere_wide4.p; v.tri_wide4 = ds.tri_wide4.p;
     fill_view_constants(v, hs, d);
     return RT_OK;
 }
@@ -151,7 +148,7 @@ struct rt_scene {
     int num_prims = 0;
     int bvh_prims = 0;              // spheres + triangles (the primitives the BVHs cover)
     bool bvh_ok = true;             // both trees fit the traversal stack (depth <= RT_BVH_STACK)
-    bool bvh4_ok = true;            // the four-child walk's stack bound fits RT_BVH4_STACK
+    bool tri_bvh = false;           // the scene has a triangle BVH (pool chunk choice)
     double record_bytes = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {};
@@ -160,7 +157,10 @@ struct rt_scene {
     DevBuf<uint8_t> rgba;
     DevBuf<uint32_t> segs, draws;
     DevBuf<unsigned long long> total;
-    DevBuf<unsigned char> pool;     // sample-pool per-sample radiance (ensure_pool)
+    DevBuf<double> part;            // sample-pool chunk partials (ensure_partials)
+    hipEvent_t scratch_ev = nullptr;   // recorded after every use of part / total (order_scratch)
+    hipStream_t scratch_stream = nullptr;
+    bool scratch_used = false;
     std::atomic<int> cancel{0};
     size_t ckpt_pixels = 0;         // progressive state of the last rt_render / rt_render_resume:
     int ckpt_done = 0;              // `sum` holds samples [sample_begin, ckpt_done) of ckpt_pixels pixels
@@ -228,38 +228,54 @@ int check_accel(const rt_scene* sc, const rt_settings* s) {
 
 hipError_t trace(rt_scene* sc, const rt_settings* s, const ImageParams& im, const Counters& c, hipStream_t st) {
     if (im.max_depth <= 0) return hipSuccess;   // rayColor(ray, depth<=0) is 0: nothing to trace
-    const int walk = !use_bvh(sc, s) ? ACC_BRUTE : (sc->bvh4_ok ? ACC_BVH4 : ACC_BVH_STACK);
-    if (s->precision == RT_PREC_F32) return launch_trace<float>(sc->s32.view, im, c, walk, st);
-    return launch_trace<double>(sc->s64.view, im, c, walk, st);
+    const bool bvh = use_bvh(sc, s);
+    if (s->precision == RT_PREC_F32) return launch_trace<float>(sc->s32.view, im, c, bvh, st);
+    return launch_trace<double>(sc->s64.view, im, c, bvh, st);
 }
 
-// Sample-pool radiance buffer (trace_uses_pool, pt_trace.hip): every sample of the call when they fit
-// the budget (RT_POOL_MB, default 32 GiB of the 288 GB HBM, at most 40 % of the free device memory),
-// else as many whole samples as fit (launch_trace then splits the samples over several launches).
-// Kept by the scene between renders.
-int ensure_pool(rt_scene* sc, const rt_settings* s, int cw, int ch, int samples, Counters& c) {
+// Sample-pool chunk partials (pool_partial_bytes, pt_trace.hip): all of a launch's chunks when they fit
+// the budget (RT_PART_MB, default 2 GiB, at most 10 % of the free device memory), else as many
+// chunks as fit (launch_trace then splits the samples over several launches).  RTOW 1080p x 512 spp
+// needs 0.8 GB; a launch with a single chunk needs none.  Kept by the scene between renders.
+int ensure_partials(rt_scene* sc, const rt_settings* s, int cw, int ch, int samples, Counters& c) {
     if (!trace_uses_pool() || samples <= 0 || cw <= 0 || ch <= 0) return RT_OK;
-    const size_t per_sample = pool_sample_bytes(cw, ch, s->precision == RT_PREC_F32 ? sizeof(float) : sizeof(double));
+    const size_t want_all = pool_partial_bytes(cw, ch, samples, sc->tri_bvh);
+    if (want_all == 0) return RT_OK;
+    const size_t per_chunk = (size_t)((cw + 7) / 8) * ((ch + 7) / 8) * kPartialBytesPerTile;
     static size_t budget = 0;
     if (!budget) {
-        const char* e = getenv("RT_POOL_MB");
-        budget = (size_t)(e ? std::max(1LL, atoll(e)) : 32768LL) << 20;
+        const char* e = getenv("RT_PART_MB");
+        budget = (size_t)(e ? std::max(1LL, atoll(e)) : 2048LL) << 20;
     }
-    size_t want = per_sample * (size_t)samples;
-    if (want > sc->pool.n) {
+    size_t want = want_all;
+    if (want > sc->part.n * sizeof(double)) {
         size_t free_b = 0, total_b = 0, cap = budget;
-        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = std::min(cap, (free_b + sc->pool.n) / 10 * 4);
-        want = std::min(want, std::max<size_t>(cap / per_sample, 1) * per_sample);
-        while (want > sc->pool.n) {
-            if (sc->pool.ensure(want) == hipSuccess) break;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = std::min(cap, (free_b + sc->part.n * sizeof(double)) / 10);
+        want = std::min(want, std::max<size_t>(cap / per_chunk, 1) * per_chunk);
+        while (want > sc->part.n * sizeof(double)) {
+            if (sc->part.ensure(want / sizeof(double)) == hipSuccess) break;
             (void)hipGetLastError();
-            if (want == per_sample) return fail(RT_ERR_DEVICE, "sample pool: cannot allocate %zu bytes", per_sample);
-            want = std::max<size_t>(want / per_sample / 2, 1) * per_sample;
+            if (want == per_chunk) return fail(RT_ERR_DEVICE, "sample pool: cannot allocate %zu bytes", per_chunk);
+            want = std::max<size_t>(want / per_chunk / 2, 1) * per_chunk;
         }
     }
-    c.pool = sc->pool.p;
-    c.pool_bytes = sc->pool.n;
+    c.part = sc->part.p;
+    c.part_bytes = sc->part.n * sizeof(double);
     return RT_OK;
+}
+
+// The scene's scratch buffers (chunk partials, work totals) are shared by every call on the scene.
+// A call on stream `st` first waits for the previous user of the scratch (possibly another stream:
+// rt_trace_device on a caller's stream, rt_render on the scene's own) and records the event again
+// when it has enqueued its last use, so asynchronous calls on different streams never overlap on it.
+hipError_t order_scratch(rt_scene* sc, hipStream_t st) {
+    if (!sc->scratch_used || sc->scratch_stream == st) return hipSuccess;
+    return hipStreamWaitEvent(st, sc->scratch_ev, 0);
+}
+hipError_t release_scratch(rt_scene* sc, hipStream_t st) {
+    sc->scratch_stream = st;
+    sc->scratch_used = true;
+    return hipEventRecord(sc->scratch_ev, st);
 }
 
 // totals = [segments, BVH nodes, sphere tests, triangle tests] of the launches
@@ -329,7 +345,7 @@ int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out) {
     sc->num_prims = hs.num_prims;
     sc->bvh_prims = (int)(hs.sphere_r.size() + hs.tri_mat.size());
     sc->bvh_ok = hs.bvh_depth <= RT_BVH_STACK;
-    sc->bvh4_ok = sc->bvh_ok && hs.bvh4_stack <= RT_BVH4_STACK;
+    sc->tri_bvh = !hs.tri_wide.empty();
     sc->record_bytes = hs.record_bytes;
     if ((rc = build_device(sc->s64, hs, *desc)) || (rc = build_device(sc->s32, hs, *desc))) {
         rt_scene_destroy(sc);
@@ -337,6 +353,7 @@ int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out) {
     }
     hipError_t e = hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking);
     for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreate(&sc->ev[k]);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&sc->scratch_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
         rt_scene_destroy(sc);
         return fail(RT_ERR_DEVICE, "stream/event create: %s", hipGetErrorString(e));
@@ -352,7 +369,8 @@ void rt_scene_destroy(rt_scene* sc) {
     sc->s64.release();
     sc->s32.release();
     sc->sum.release(); sc->mean.release(); sc->post.release(); sc->post_raw.release(); sc->rgba.release();
-    sc->segs.release(); sc->draws.release(); sc->total.release(); sc->pool.release();
+    sc->segs.release(); sc->draws.release(); sc->total.release(); sc->part.release();
+    if (sc->scratch_ev) (void)hipEventDestroy(sc->scratch_ev);
     for (auto& e : sc->ev)
         if (e) (void)hipEventDestroy(e);
     if (sc->stream) (void)hipStreamDestroy(sc->stream);
@@ -384,10 +402,11 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     const bool want_segs = out && out->segments, want_draws = out && out->draws;
     HIP_TRY(sc->sum.ensure(3 * n));
     HIP_TRY(sc->total.ensure(kTotalSlots));
+    HIP_TRY(order_scratch(sc, sc->stream));
     if (sums_in) HIP_TRY(hipMemcpyAsync(sc->sum.p, sums_in, 3 * n * sizeof(double), hipMemcpyHostToDevice, sc->stream));
     else HIP_TRY(hipMemsetAsync(sc->sum.p, 0, 3 * n * sizeof(double), sc->stream));
     HIP_TRY(hipMemsetAsync(sc->total.p, 0, kTotalSlots * sizeof(unsigned long long), sc->stream));
-    Counters c{sc->sum.p, nullptr, nullptr, sc->total.p, sc->total.p + kQueueSlot};
+    Counters c{sc->sum.p, nullptr, nullptr, sc->total.p};
     if (want_segs) {
         HIP_TRY(sc->segs.ensure(n));
         HIP_TRY(hipMemsetAsync(sc->segs.p, 0, n * sizeof(uint32_t), sc->stream));
@@ -402,7 +421,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     im.s_begin = std::max(im.s_begin, first);
     const int s0 = im.s_begin, s1 = std::max(im.s_end, s0);
     const int batch = s->batch_samples > 0 ? s->batch_samples : std::max(1, s1 - s0);
-    if (s->max_depth > 0 && (rc = ensure_pool(sc, s, cw, ch, std::min(batch, s1 - s0), c))) return rc;
+    if (s->max_depth > 0 && (rc = ensure_partials(sc, s, cw, ch, std::min(batch, s1 - s0), c))) return rc;
     sc->ckpt_pixels = n;
     sc->ckpt_done = s0;
     double kernel_ms = 0;
@@ -438,6 +457,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     if (want_draws) HIP_TRY(hipMemcpyAsync(out->draws, sc->draws.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, sc->stream));
     unsigned long long totals[kTotalSlots] = {};
     HIP_TRY(hipMemcpyAsync(totals, sc->total.p, sizeof totals, hipMemcpyDeviceToHost, sc->stream));
+    HIP_TRY(release_scratch(sc, sc->stream));
     HIP_TRY(hipStreamSynchronize(sc->stream));
     if (stats) {
         float fms = 0;
@@ -501,16 +521,18 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
     // accumulate pass)
     hipStream_t st = (hipStream_t)hip_stream;
     HIP_TRY(sc->total.ensure(kTotalSlots));
-    HIP_TRY(hipMemsetAsync(sc->total.p, 0, kTotalSlots * sizeof(unsigned long long), st));
     ImageParams im = image_params(s, cw, ch);
-    Counters c{d_sum, nullptr, nullptr, sc->total.p, sc->total.p + kQueueSlot};
-    if (s->max_depth > 0 && (rc = ensure_pool(sc, s, cw, ch, im.s_end - im.s_begin, c))) return rc;
+    Counters c{d_sum, nullptr, nullptr, sc->total.p};
+    if (s->max_depth > 0 && (rc = ensure_partials(sc, s, cw, ch, im.s_end - im.s_begin, c))) return rc;
+    HIP_TRY(order_scratch(sc, st));
+    HIP_TRY(hipMemsetAsync(sc->total.p, 0, kTotalSlots * sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(sc->ev[0], st));
     HIP_TRY(trace(sc, s, im, c, st));
     HIP_TRY(hipEventRecord(sc->ev[1], st));
+    unsigned long long totals[kTotalSlots] = {};
+    if (sync || stats) HIP_TRY(hipMemcpyAsync(totals, sc->total.p, sizeof totals, hipMemcpyDeviceToHost, st));
+    HIP_TRY(release_scratch(sc, st));
     if (sync || stats) {
-        unsigned long long totals[kTotalSlots] = {};
-        HIP_TRY(hipMemcpyAsync(totals, sc->total.p, sizeof totals, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         if (stats) {
             float ms = 0;

@@ -23,10 +23,8 @@ struct HostScene {   // precision-independent staging, binary64 as packed by the
     std::vector<double> tri_verts;                                // v0, v1, v2 as given (BVH bounds)
     std::vector<BvhNode> sphere_bvh, tri_bvh;                     // built by build_bvhs()
     std::vector<int> sphere_bvh_prims, tri_bvh_prims;
-    std::vector<WideNode> sphere_wide, tri_wide;                  // the same trees, two-child nodes
+    std::vector<Bvh2Node> sphere_wide, tri_wide;                  // the same trees, two-child nodes
     int bvh_depth = 0;                                            // deepest leaf of either tree
-    std::vector<Bvh4Node> sphere_wide4, tri_wide4;                // four-child collapse of the trees
-    int bvh4_stack = 0;                                           // their worst traversal-stack use
     int num_prims = 0;
     double record_bytes = 0;      // SURVEY §8d canonical bytes tested per segment
 };
@@ -334,100 +332,6 @@ inline std::vector<Bvh2Node> make_wide(const std::vector<BvhNode>& t) {
     return out;
 }
 
-// binary32 -> binary16 rounded toward +inf (up) or -inf (down): the result bounds x on that side
-inline _Float16 f16_toward(float x, bool up) {
-    _Float16 h = (_Float16)x;
-    const float back = (float)h;
-    if (x != x || (up ? back >= x : back <= x)) return h;
-    uint16_t u;
-    memcpy(&u, &h, 2);
-    if ((u & 0x7FFF) == 0) u = up ? 0x0001 : 0x8001;            // +-0 -> smallest subnormal
-    else if (!(u & 0x8000)) u = up ? (uint16_t)(u + 1) : (uint16_t)(u - 1);
-    else u = up ? (uint16_t)(u - 1) : (uint16_t)(u + 1);
-    memcpy(&h, &u, 2);
-    return h;
-}
-
-// Bvh2Node -> Bvh2NodeH: lower bounds rounded down, upper bounds up (pt_core.h)
-inline Bvh2NodeH to_half_node(const Bvh2Node& n) {
-    Bvh2NodeH h{};
-    for (int a = 0; a < 3; ++a)
-        for (int c = 0; c < 2; ++c) {
-            h.lo[a][c] = f16_toward(n.lo[a][c], false);
-            h.hi[a][c] = f16_toward(n.hi[a][c], true);
-        }
-    h.child[0] = n.child[0];
-    h.child[1] = n.child[1];
-    return h;
-}
-
-inline std::vector<WideNode> make_wide_nodes(const std::vector<BvhNode>& t) {
-    const std::vector<Bvh2Node> w = make_wide(t);
-#if RT_BVH_HALF
-    std::vector<WideNode> out;
-    out.reserve(w.size());
-    for (const Bvh2Node& n : w) out.push_back(to_half_node(n));
-    return out;
-#else
-    return w;
-#endif
-}
-
-// preorder BvhNode tree -> Bvh4Node array (root first, preorder): each four-child node takes its
-// binary node's two children and opens the inner child of largest surface area until it has four.
-// Returns the largest traversal-stack use of the ordered walk (a node pushes up to children-1
-// entries), so the caller can check it against RT_BVH_STACK.
-inline int make_wide4(const std::vector<BvhNode>& t, std::vector<Bvh4Node>& out) {
-    out.clear();
-    if (t.empty()) return 0;
-    auto area = [&](int i) {
-        const double x = (double)t[i].hi[0] - t[i].lo[0], y = (double)t[i].hi[1] - t[i].lo[1],
-                     z = (double)t[i].hi[2] - t[i].lo[2];
-        const double a = x * y + y * z + z * x;
-        return a == a ? a : INFINITY;
-    };
-    struct Rec {
-        static int build(const std::vector<BvhNode>& t, std::vector<Bvh4Node>& out, int root,
-                         const decltype(area)& area) {   // returns the max stack use below this node
-            std::vector<int> kids;
-            if (t[root].fc != 0) kids.push_back(root);   // a single-leaf tree
-            else { kids.push_back(root + 1); kids.push_back(t[root + 1].skip); }
-            while (kids.size() < 4) {
-                int best = -1;
-                double ba = -1;
-                for (size_t k = 0; k < kids.size(); ++k)
-                    if (t[kids[k]].fc == 0 && area(kids[k]) > ba) { ba = area(kids[k]); best = (int)k; }
-                if (best < 0) break;
-                const int n = kids[best];
-                kids[best] = n + 1;
-                kids.insert(kids.begin() + best + 1, t[n + 1].skip);
-            }
-            const int me = (int)out.size();
-            out.push_back(Bvh4Node{});
-            Bvh4Node node{};
-            int deepest = 0;
-            for (int k = 0; k < 4; ++k) {
-                if (k >= (int)kids.size()) {
-                    node.child[k] = RT_CHILD_EMPTY;
-                    for (int a = 0; a < 3; ++a) { node.lo[a][k] = 0; node.hi[a][k] = 0; }
-                    continue;
-                }
-                const int c = kids[k];
-                for (int a = 0; a < 3; ++a) { node.lo[a][k] = t[c].lo[a]; node.hi[a][k] = t[c].hi[a]; }
-                if (t[c].fc != 0) {
-                    node.child[k] = ~t[c].fc;
-                } else {
-                    node.child[k] = (int)out.size();
-                    deepest = std::max(deepest, build(t, out, c, area));
-                }
-            }
-            out[me] = node;
-            return (int)kids.size() - 1 + deepest;
-        }
-    };
-    return Rec::build(t, out, 0, area);
-}
-
 inline void build_bvhs(HostScene& hs) {
     BvhBuilder sb;
     for (size_t i = 0; i < hs.sphere_r.size(); ++i) {
@@ -460,9 +364,8 @@ inline void build_bvhs(HostScene& hs) {
     hs.bvh_depth = std::max(hs.bvh_depth, tb.max_depth);
     hs.tri_bvh = std::move(tb.nodes);
     hs.tri_bvh_prims = std::move(tb.order);
-    hs.sphere_wide = make_wide_nodes(hs.sphere_bvh);
-    hs.tri_wide = make_wide_nodes(hs.tri_bvh);
-    hs.bvh4_stack = std::max(make_wide4(hs.sphere_bvh, hs.sphere_wide4), make_wide4(hs.tri_bvh, hs.tri_wide4));
+    hs.sphere_wide = make_wide(hs.sphere_bvh);
+    hs.tri_wide = make_wide(hs.tri_bvh);
 }
 
 // Record arrays of one precision (host memory); rt_capi.cpp uploads them, tests/hostcheck uses them.
@@ -554,6 +457,7 @@ void fill_view_constants(SceneView<R>& v, const HostScene& hs, const rt_scene_de
     v.num_tri_nodes = (int)hs.tri_bvh.size();
     v.num_sphere_wide = (int)hs.sphere_wide.size();
     v.num_tri_wide = (int)hs.tri_wide.size();
+    v.stack_entries = std::max(1, hs.bvh_depth);
     const rt_camera_desc& c = d.camera;
     for (int k = 0; k < 3; ++k) {
         v.cam_o[k] = (R)c.origin[k];

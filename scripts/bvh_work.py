@@ -21,8 +21,8 @@ cfg = dict(bench.CONFIGS[cfg_name], spp=spp)
 rt = bench.make_tracer(cfg, "f64", 1, 0)
 L = hb.lib(defs)
 L.ptc_work.argtypes = [C.POINTER(capi.SceneDesc), C.POINTER(capi.Settings), C.POINTER(C.c_double)]
-out = (C.c_double * 8)()
-tot = [0.0] * 8
+out = (C.c_double * 4)()
+tot = [0.0] * 4
 # a few crops spread over the frame
 for (fx, fy) in ((0.5, 0.5), (0.25, 0.7), (0.75, 0.3), (0.5, 0.9), (0.1, 0.2)):
     x0, y0 = int(fx * (cfg["w"] - side)), int(fy * (cfg["h"] - side))
@@ -31,5 +31,4 @@ for (fx, fy) in ((0.5, 0.5), (0.25, 0.7), (0.75, 0.3), (0.5, 0.9), (0.1, 0.2)):
     tot = [a + b for a, b in zip(tot, out)]
 seg = tot[0]
 print(f"{cfg_name} {defs}: segments {seg:.0f}, nodes/seg {tot[1]/seg:.3f}, spheres/seg {tot[2]/seg:.3f}, "
-      f"tris/seg {tot[3]/seg:.3f}, f64/seg {tot[4]/seg:.3f}, away/seg {tot[5]/seg:.3f}, cand/seg {tot[6]/seg:.3f}, "
-      f"better/seg {tot[7]/seg:.3f}")
+      f"tris/seg {tot[3]/seg:.3f}")

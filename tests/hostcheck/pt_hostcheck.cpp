@@ -29,9 +29,8 @@ struct HostView {
         v.sphere_nodes = hs.sphere_bvh.data(); v.tri_nodes = hs.tri_bvh.data();
         v.bvh_sphere_leaf = rec.bvh_sphere_leaf.data(); v.bvh_tri_leaf = rec.bvh_tri_leaf.data();
         v.sphere_wide = hs.sphere_wide.data(); v.tri_wide = hs.tri_wide.data();
-        v.sphere_wide4 = hs.sphere_wide4.data(); v.tri_wide4 = hs.tri_wide4.data();
         fill_view_constants(v, hs, *d);
-        return hs.bvh4_stack <= 64;                  // the host walks use 64-entry stacks
+        return hs.bvh_depth <= 64;                   // the host walks use 64-entry stacks
     }
 };
 
@@ -53,29 +52,16 @@ static int render(const rt_scene_desc* d, const rt_settings* s, double* sum, uin
     im.seedm = host_seed_mix(s->seed);
     int stack[64];
     const BvhStack stk{stack, 1};
-    const LdsSpheres no_lds{nullptr};
-#if PTC_QUEUE
-    // the pixel-queue loop (RT_PIXEL_QUEUE kernels), one lane taking every pixel in queue order
-    if (im.max_depth <= 0) return 0;
-    uint32_t head = 0;
-    auto fetch = [&head]() { return head++; };
-    if (s->accel == RT_ACCEL_BVH) trace_pixels_queue<R, true, ACC_BVH4>(v, im, fetch, sum, segs, draws, no_lds, stk);
-    else if (s->accel == 3) trace_pixels_queue<R, true, ACC_BVH>(v, im, fetch, sum, segs, draws, no_lds, stk);
-    else if (s->accel == 4) trace_pixels_queue<R, true, ACC_BVH_STACK>(v, im, fetch, sum, segs, draws, no_lds, stk);
-    else trace_pixels_queue<R, true, ACC_BRUTE>(v, im, fetch, sum, segs, draws, no_lds, stk);
-    return 0;
-#endif
     for (int cy = 0; cy < im.ch; ++cy)
         for (int cx = 0; cx < im.cw; ++cx) {
             const size_t q = (size_t)cy * im.cw + cx;
             PixelResult r{0, 0, {0, 0, 0}};
             double* acc = sum + 3 * q;
-            // accel: RT_ACCEL_BVH = the four-child walk; hostcheck-only selectors 3 = the stackless
-            // walk, 4 = the two-child walk
+            // accel: RT_ACCEL_BVH = the ordered two-child walk (the kernel's); hostcheck-only
+            // selector 3 = the stackless preorder walk
             if (im.max_depth > 0)
-                r = s->accel == RT_ACCEL_BVH ? trace_pixel<R, true, ACC_BVH4>(v, im, cx, cy, im.s_end, acc, no_lds, stk)
+                r = s->accel == RT_ACCEL_BVH ? trace_pixel<R, true, ACC_BVH_STACK>(v, im, cx, cy, im.s_end, acc, stk)
                   : s->accel == 3            ? trace_pixel<R, true, ACC_BVH>(v, im, cx, cy, im.s_end, acc)
-                  : s->accel == 4            ? trace_pixel<R, true, ACC_BVH_STACK>(v, im, cx, cy, im.s_end, acc, no_lds, stk)
                                              : trace_pixel<R, true, ACC_BRUTE>(v, im, cx, cy, im.s_end, acc);
             segs[q] = r.segments;
             draws[q] = r.draws;
@@ -192,15 +178,13 @@ extern "C" long long ptc_bvh_check(const rt_scene_desc* d, long long n, unsigned
         }
         const double dl = std::pow(10.0, 2.0 * U(gen));
         V3<double> O{o[0], o[1], o[2]}, D{(target[0] - o[0]) * dl, (target[1] - o[1]) * dl, (target[2] - o[2]) * dl};
-        const Closest<double> a = closest_hit<double, false>(v, O, D);
+        const Closest<double> a = closest_hit<double>(v, O, D);
         Work w{0, 0, 0};
         int stack[RT_BVH_STACK];
-        int stack4[64];
-        const Closest<double> b = closest_hit_bvh<double, 0>(v, O, D, w, BvhStack{nullptr, 0});
-        const Closest<double> c = closest_hit_bvh<double, 1>(v, O, D, w, BvhStack{stack, 1});
-        const Closest<double> e = closest_hit_bvh<double, 2>(v, O, D, w, BvhStack{stack4, 1});
+        const Closest<double> b = closest_hit_bvh<double, false>(v, O, D, w, BvhStack{nullptr, 0});
+        const Closest<double> c = closest_hit_bvh<double, true>(v, O, D, w, BvhStack{stack, 1});
         if (a.kind != HIT_NONE) ++nh;
-        for (const Closest<double>& x : {b, c, e}) {
+        for (const Closest<double>& x : {b, c}) {
             const bool same = a.kind == x.kind && (a.kind == HIT_NONE || (a.idx == x.idx && a.mat == x.mat &&
                                                                          std::memcmp(&a.t, &x.t, 8) == 0));
             bad += !same;
@@ -210,19 +194,17 @@ extern "C" long long ptc_bvh_check(const rt_scene_desc* d, long long n, unsigned
     return bad;
 }
 
-// BVH shape: deepest leaf of the binary trees and the four-child walk's worst stack use
-extern "C" int ptc_bvh_info(const rt_scene_desc* d, int* depth, int* stack4, int* nodes2, int* nodes4) {
+// BVH shape: deepest leaf of the binary trees and their two-child node count
+extern "C" int ptc_bvh_info(const rt_scene_desc* d, int* depth, int* nodes2) {
     HostView<double> hv;
     hv.init(d);
     *depth = hv.hs.bvh_depth;
-    *stack4 = hv.hs.bvh4_stack;
     *nodes2 = (int)(hv.hs.sphere_wide.size() + hv.hs.tri_wide.size());
-    *nodes4 = (int)(hv.hs.sphere_wide4.size() + hv.hs.tri_wide4.size());
     return 0;
 }
 
 // Work totals of the two-child walk over a crop (host experiments on BVH quality, TEST/DEV TOOL):
-// out = {segments, nodes, sphere tests, triangle tests, x0..x3 (RT_WORK_EXTRA)}
+// out = {segments, nodes, sphere tests, triangle tests}
 extern "C" int ptc_work(const rt_scene_desc* d, const rt_settings* s, double* out) {
     HostView<double> hv;
     if (!hv.init(d)) return -1;
@@ -239,13 +221,12 @@ extern "C" int ptc_work(const rt_scene_desc* d, const rt_settings* s, double* ou
     im.seedm = host_seed_mix(s->seed);
     int stack[64];
     const BvhStack stk{stack, 1};
-    for (int k = 0; k < 8; ++k) out[k] = 0;
+    for (int k = 0; k < 4; ++k) out[k] = 0;
     for (int cy = 0; cy < im.ch; ++cy)
         for (int cx = 0; cx < im.cw; ++cx) {
             double acc[3] = {0, 0, 0};
-            const PixelResult r = trace_pixel<double, true, ACC_BVH_STACK>(hv.v, im, cx, cy, im.s_end, acc, LdsSpheres{nullptr}, stk);
+            const PixelResult r = trace_pixel<double, true, ACC_BVH_STACK>(hv.v, im, cx, cy, im.s_end, acc, stk);
             out[0] += r.segments; out[1] += r.work.nodes; out[2] += r.work.spheres; out[3] += r.work.tris;
-            for (int k = 0; k < 4; ++k) out[4 + k] += r.work.x[k];
         }
     return 0;
 }

@@ -32,7 +32,7 @@ def _bind(L):
                              C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.ptc_bvh_check.argtypes = [C.POINTER(capi.SceneDesc), C.c_longlong, C.c_uint, C.POINTER(C.c_longlong)]
     L.ptc_bvh_check.restype = C.c_longlong
-    L.ptc_bvh_info.argtypes = [C.POINTER(capi.SceneDesc)] + [C.POINTER(C.c_int)] * 4
+    L.ptc_bvh_info.argtypes = [C.POINTER(capi.SceneDesc)] + [C.POINTER(C.c_int)] * 2
     return L
 
 
@@ -47,8 +47,8 @@ def lib(defines=()):
 
 
 def bvh_info(packed, L=None):
-    """(deepest leaf of the binary trees, four-child walk stack bound, two-child nodes, four-child nodes)"""
-    v = [C.c_int() for _ in range(4)]
+    """(deepest leaf of the binary trees, two-child nodes)"""
+    v = [C.c_int() for _ in range(2)]
     (L or lib()).ptc_bvh_info(C.byref(packed.desc), *[C.byref(x) for x in v])
     return tuple(x.value for x in v)
 

@@ -58,7 +58,7 @@ if (cmd === 'pack') {
     summary._render = { progress: seen, nonzero: rt.imageData.data.some((v, i) => i % 4 !== 3 && v > 0) };
     // progressive: window.renderCancelled mid-frame, then resume() from the checkpoint
     {
-        const { rt: full } = tracerFor('kitchen_sink');
+        const { rt: full } = tracerFor('kitchen_sink', { batchSamples: 2 });   // same sample batches
         full.updateRenderSettings({ samples: 8 });
         await full.render();
         const { rt: part } = tracerFor('kitchen_sink', { batchSamples: 2 });

@@ -44,30 +44,14 @@ def test_kernel_logic_f32_close_to_oracle():
     assert np.sqrt(np.mean((r["mean"] - o["mean"]) ** 2)) < 0.05
 
 
-@pytest.mark.parametrize("walk", ["four-child", "two-child", "stackless"])
+@pytest.mark.parametrize("walk", ["two-child", "stackless"])
 @pytest.mark.parametrize("case", gc.case_names())
 def test_kernel_logic_bvh_matches_reference(case, walk):
-    """RT_ACCEL_BVH (closest_hit_bvh: the ordered four- and two-child walks and the stackless walk)
-    gives the same decisions as World.hit on every golden case."""
+    """RT_ACCEL_BVH (closest_hit_bvh: the ordered two-child walk of the kernel, and the stackless
+    preorder walk) gives the same decisions as World.hit on every golden case."""
     rt, c = gc.tracer_for(case)
-    rt.accel = {"four-child": capi.RT_ACCEL_BVH, "stackless": 3, "two-child": 4}[walk]   # 3, 4: hostcheck-only
+    rt.accel = {"two-child": capi.RT_ACCEL_BVH, "stackless": 3}[walk]   # 3: hostcheck-only
     r = hb.render(rt.packed(), rt.settings(crop=c["crop"]))
-    assert np.array_equal(r["segments"], gc.load_array(case, "segs"))
-    assert np.array_equal(r["draws"], gc.load_array(case, "draws"))
-    lin = gc.load_array(case, "linear")
-    assert np.array_equal(np.isnan(r["mean"]), np.isnan(lin))
-    ok = ~np.isnan(lin)
-    assert np.all(np.abs(r["mean"][ok] - lin[ok]) <= 1e-12 * np.maximum(1, np.abs(lin[ok])))
-
-
-@pytest.mark.parametrize("accel", [0, 4])
-@pytest.mark.parametrize("case", gc.case_names())
-def test_pixel_queue_loop_matches_reference(case, accel):
-    """trace_pixels_queue (the RT_PIXEL_QUEUE kernels' loop: a lane moves on to the next queued pixel
-    when its pixel is done) gives every pixel exactly trace_pixel's samples, segments and draws."""
-    rt, c = gc.tracer_for(case)
-    rt.accel = accel
-    r = hb.render(rt.packed(), rt.settings(crop=c["crop"]), hb.lib(("PTC_QUEUE=1",)))
     assert np.array_equal(r["segments"], gc.load_array(case, "segs"))
     assert np.array_equal(r["draws"], gc.load_array(case, "draws"))
     lin = gc.load_array(case, "linear")
