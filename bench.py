@@ -1,16 +1,20 @@
 """Benchmark of the path-tracing hot path (BASELINE.json metric) on 1..8 MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config rtow|cornell|rtow4k|mesh50k|sample_scene]
-                    [--precision f64|f32] [--no-cpu-baseline] [--no-end-to-end]
+                    [--precision f64|f32] [--no-cpu-baseline] [--no-end-to-end] [--no-pmc]
 
 A "step" renders one full frame of the workload: every pixel x every sample, traced on the GPU(s)
 from a scene already resident in HBM, the per-pixel float64 sums RCCL-reduced to rank 0 (N>1), and
 the epilogue (mean, tone map, gamma, RGBA8) run on rank 0's GPU.  Rank r traces samples
 [r*S/N, (r+1)*S/N) of every pixel, so the frame is fixed as N grows ("scaling": "strong").
 
-Prints ONE JSON line on rank 0 (driver contract).  `roofline` is computed from HIP events recorded
-inside librt_hip.so on the stream the trace kernel runs on; `cpu_baseline` times the CPU oracle
-(oracle/pt_oracle.c, 1 thread, the JS semantics in C) on a bounded crop of the same workload.
+Prints ONE JSON line on rank 0 (driver contract).  The trace step's duration comes from HIP events
+recorded inside librt_hip.so on the stream the kernels run on.  At N=1 (unless --no-pmc) rank 0 then
+re-runs one frame of the same workload under rocprofv3 three times — FETCH_SIZE, WRITE_SIZE and eight
+SQ counters, each pass in its own process — so `roofline` (measured HBM bytes, bound "hbm") and
+`roofline_binding` (VALU issue slots and lane utilization, the resource that binds) are measured by
+this run, at this commit.  `cpu_baseline` times the CPU restatements on a bounded crop of the same
+workload on this host.
 """
 import argparse
 import ctypes as C
@@ -58,6 +62,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-end-to-end", action="store_true", help="skip the PCIe-inclusive rt_render timing")
     ap.add_argument("--cpu-crop", type=int, default=64, help="side of the square crop the CPU oracle renders")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 counter passes (N=1 roofline)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -91,32 +97,70 @@ def cpu_baseline(rt, cfg, side):
                       f"maxDepth {cfg['depth']}: {samples} samples in {dt:.1f} s (oracle/pt_oracle.c, 1 thread)"}
 
 
-def load_traffic(workload, precision):
-    """HBM bytes per trace step (trace_pool_kernel + accumulate_kernel) from the rocprofv3 PMC passes
-    (profiles/pmc_<workload>_<prec>.json, written by scripts/profile_round.sh)."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{workload}_{precision}.json")
-    if os.path.exists(p):
-        with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
-    return None
-
-
 # VALU issue ceiling: 256 CUs x 4 SIMD-32s, a wave64 VALU instruction holds its SIMD for 2 cycles (a
 # binary64 one for 4: FP64 vector is half the FP32 rate) at 2.4 GHz (MI355X_MICROARCH.md)
 VALU_ISSUE_PEAK_GSLOTS = 256 * 4 * 2.4 / 2
+TRACE_KERNELS = ("trace_pool_kernel", "reduce_kernel")   # the trace step: one launch each per frame
+SQ_COUNTERS = ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_INSTS_VALU_ADD_F64",
+               "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")
 
 
-def load_sq(workload, precision):
-    """SQ counters of one trace step (profiles/sq_<workload>_<prec>.json, scripts/profile_round.sh)."""
-    p = os.path.join(ROOT, "profiles", f"sq_{workload}_{precision}.json")
-    if os.path.exists(p):
-        with open(p) as f:
-            return json.load(f)
-    return None
+def pmc_child(args):
+    """--pmc-child: one frame of the workload through rt_render (the same trace launches as a bench
+    step), run under rocprofv3 --pmc by pmc_passes()."""
+    rt = make_tracer(CONFIGS[args.config], args.precision, args.seed, 0, args.accel)
+    rt.render()
+    rt.close()
+
+
+def pmc_passes(args, outdir):
+    """rocprofv3 --pmc passes (one counter group per process, as MI355X_MICROARCH.md prescribes) over
+    one frame; returns {counter: value summed over the trace step's kernels} per pass, or an error."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", args.config, "--precision",
+             args.precision, "--seed", str(args.seed), "--accel", args.accel]
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    res = {}
+    for name, counters in (("fetch", ("FETCH_SIZE",)), ("write", ("WRITE_SIZE",)), ("sq", SQ_COUNTERS)):
+        d = os.path.join(outdir, name)
+        cmd = ["timeout", "-s", "KILL", "240", prof, "--pmc", *counters, "--output-format", "csv", "-d", d, "-o", "run",
+               "--", *child]
+        r = subprocess.run(cmd, capture_output=True, text=True, env=env)
+        if r.returncode != 0:
+            return {"error": f"{name} pass exit {r.returncode}: {r.stderr[-300:]}"}
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if not files:
+            return {"error": f"{name} pass wrote no counter_collection.csv"}
+        tot, per_kernel = {}, {}
+        for row in csv.DictReader(open(files[0])):
+            k = next((k for k in TRACE_KERNELS if k in row["Kernel_Name"]), None)
+            if k is None:
+                continue
+            v = float(row["Counter_Value"])
+            tot[row["Counter_Name"]] = tot.get(row["Counter_Name"], 0.0) + v
+            per_kernel.setdefault(k, {})
+            per_kernel[k][row["Counter_Name"]] = per_kernel[k].get(row["Counter_Name"], 0.0) + v
+        res[name] = {"total": tot, "per_kernel": per_kernel, "csv": os.path.relpath(files[0], ROOT)}
+    return res
+
+
+def git_head():
+    try:
+        import subprocess
+        return subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
+                              timeout=10).stdout.strip() or None
+    except Exception:
+        return None
 
 
 def main():
     args = parse()
+    if args.pmc_child:
+        return pmc_child(args)
     cfg = CONFIGS[args.config]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -175,7 +219,6 @@ def main():
         value = total_samples / elapsed / 1e6
         k_ms = sum(kernel_ms) / len(kernel_ms)
         a_bytes = sum(abytes) / len(abytes)
-        achieved = a_bytes / (k_ms * 1e-3) / 1e9
         seg_launch = sum(segs) / len(segs)
         nodes, sph, tri = (sum(w[k] for w in work) / len(work) for k in range(3))
         bvh = nodes > 0
@@ -185,18 +228,57 @@ def main():
         else:
             flops = seg_launch * flops_per_segment
         rank_samples = cfg["w"] * cfg["h"] * (job.range[1] - job.range[0])
-        traffic = load_traffic(args.config, args.precision)
-        sq = load_sq(args.config, args.precision)
-        issue = None
-        if sq and world == 1:
-            slots = sq["valu_issue_slots"]
-            gslots = slots / (k_ms * 1e-3) / 1e9
-            issue = {"valu_insts_per_launch": sq["counters"]["SQ_INSTS_VALU"], "issue_slots_per_launch": slots,
-                     "achieved": round(gslots, 1), "peak": VALU_ISSUE_PEAK_GSLOTS,
-                     "unit": "G issue slots/s (wave64 VALU instruction = 1 slot, binary64 = 2)",
-                     "frac": round(gslots / VALU_ISSUE_PEAK_GSLOTS, 4),
-                     "lane_utilization": round(sq["valu_lane_utilization"], 4),
-                     "source": f"profiles/sq_{args.config}_{args.precision}.json (rocprofv3 SQ counters) / this run's kernel_ms"}
+        kernel_desc = "trace step: trace_pool_kernel + reduce_kernel (one launch each per frame)"
+        roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                    "traffic": None, "kernel": kernel_desc, "kernel_ms": round(k_ms, 3)}
+        binding = None
+        if world == 1 and not args.no_pmc:
+            import tempfile
+            keep = os.environ.get("BENCH_PMC_KEEP")      # scripts/profile_round.sh keeps the counter CSVs
+            if keep:
+                pmc = pmc_passes(args, keep)
+            else:
+                with tempfile.TemporaryDirectory(prefix="bench_pmc_", dir=os.environ.get("TMPDIR", "/tmp")) as d:
+                    pmc = pmc_passes(args, d)
+            if "error" in pmc:
+                roofline["pmc_error"] = pmc["error"]
+            else:
+                fetch = 2.0 * pmc["fetch"]["total"].get("FETCH_SIZE", 0.0) * 1024   # gfx950: x2, KiB
+                write = pmc["write"]["total"].get("WRITE_SIZE", 0.0) * 1024
+                hbm = fetch + write
+                gbs = hbm / (k_ms * 1e-3) / 1e9
+                roofline.update({"achieved": round(gbs, 3), "frac": round(gbs / HBM_PEAK_GBS, 6), "traffic": hbm,
+                                 "traffic_read": fetch, "traffic_write": write,
+                                 "counters_per_kernel": {k: {**pmc["fetch"]["per_kernel"].get(k, {}),
+                                                             **pmc["write"]["per_kernel"].get(k, {})}
+                                                         for k in TRACE_KERNELS},
+                                 "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes over one "
+                                           "frame run by this bench invocation (FETCH x2 per the gfx950 correction, "
+                                           "KiB x1024) / this run's HIP-event trace-step time",
+                                 "commit": git_head()})
+                sq = pmc["sq"]["total"]
+                f64 = sum(sq.get(f"SQ_INSTS_VALU_{k}_F64", 0.0) for k in ("ADD", "MUL", "FMA", "TRANS"))
+                slots = sq.get("SQ_INSTS_VALU", 0.0) + f64
+                gslots = slots / (k_ms * 1e-3) / 1e9
+                binding = {"bound": "valu_issue", "achieved": round(gslots, 1), "peak": VALU_ISSUE_PEAK_GSLOTS,
+                           "unit": "G issue slots/s (wave64 VALU instruction = 1 slot, binary64 = 2)",
+                           "frac": round(gslots / VALU_ISSUE_PEAK_GSLOTS, 4),
+                           "lane_utilization": round(sq["SQ_THREAD_CYCLES_VALU"] / (64.0 * sq["SQ_ACTIVE_INST_VALU"]), 4)
+                           if sq.get("SQ_ACTIVE_INST_VALU") else None,
+                           "valu_insts_per_launch": sq.get("SQ_INSTS_VALU"), "f64_insts_per_launch": f64,
+                           "waves_per_launch": sq.get("SQ_WAVES"),
+                           "source": "rocprofv3 --pmc SQ_* pass over one frame run by this bench invocation / this "
+                                     "run's HIP-event trace-step time"}
+        roofline.update({
+            "cache_served_bytes": a_bytes,
+            "cache_served_GBps": round(a_bytes / (k_ms * 1e-3) / 1e9, 2),
+            "cache_served_definition": ("SURVEY 8d algorithmic bytes, BVH form: 64 B/node visited + 16 B/sphere + "
+                                        "36 B/triangle tested + segments x 24 B/plane|box + 12 B/pixel; read from "
+                                        "L1/L2 (the trees are cache-resident), not HBM" if bvh else
+                                        "SURVEY 8d algorithmic bytes: segments x sum(prim record bytes: sphere 16, "
+                                        "plane 24, box 24, tri 36) + 12 B/pixel; scalar (SGPR) loads, not HBM"),
+            "bvh_nodes_per_segment": round(nodes / seg_launch, 3) if bvh else None,
+            "prim_tests_per_segment": round((sph + tri) / seg_launch, 3) if bvh else None})
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -206,22 +288,12 @@ def main():
                        "scene": cfg["scene"], "width": cfg["w"], "height": cfg["h"], "spp": cfg["spp"],
                        "max_depth": cfg["depth"], "primitives": packed.primitives_per_segment(), "accel": args.accel,
                        "parallelism": f"sample-split x{world} + RCCL reduce" if world > 1 else "1 GPU"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
-                         "kernel": "trace_pool_kernel + accumulate_kernel (one launch each per frame)",
-                         "kernel_ms": round(k_ms, 3),
-                         "algorithmic_bytes_per_launch": a_bytes,
-                         "definition": ("BVH: 64 B/node visited + 16 B/sphere + 36 B/triangle tested + segments x "
-                                        "24 B/plane|box + 12 B/pixel" if bvh else
-                                        "segments x sum(prim record bytes: sphere 16, plane 24, box 24, tri 36) "
-                                        "+ 12 B/pixel (SURVEY 8d); served from SGPR/L1, not HBM"),
-                         "bvh_nodes_per_segment": round(nodes / seg_launch, 3) if bvh else None,
-                         "prim_tests_per_segment": round((sph + tri) / seg_launch, 3) if bvh else None},
-            "valu": {"achieved": round(flops / (k_ms * 1e-3) / 1e12, 3), "peak": VALU_PEAK_TFLOPS[args.precision],
-                     "unit": "TFLOP/s", "frac": round(flops / (k_ms * 1e-3) / 1e12 / VALU_PEAK_TFLOPS[args.precision], 4),
-                     "flops_per_segment": round(flops / seg_launch, 2)},
-            "valu_issue": issue,
+            "roofline": roofline,
+            "roofline_binding": binding,
+            "valu_flops": {"achieved": round(flops / (k_ms * 1e-3) / 1e12, 3), "peak": VALU_PEAK_TFLOPS[args.precision],
+                           "unit": "TFLOP/s", "frac": round(flops / (k_ms * 1e-3) / 1e12 / VALU_PEAK_TFLOPS[args.precision], 4),
+                           "flops_per_segment": round(flops / seg_launch, 2),
+                           "definition": "SURVEY 8d canonical flops (12/node, 23/sphere, 51/triangle test)"},
             "segments_per_sample": round(seg_launch / rank_samples, 4),
             "kernel_msamples_per_s": round(rank_samples / (k_ms * 1e-3) / 1e6, 3),
             "cpu_baseline": cpu,

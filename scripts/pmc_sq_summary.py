@@ -1,5 +1,5 @@
 """SQ counters of the trace step (trace_pool_kernel + accumulate_kernel, one launch each) from one
-rocprofv3 --pmc pass -> profiles/sq_<workload>_<prec>.json, read by bench.py for `valu_issue`.
+rocprofv3 --pmc pass -> profiles/r01_final_sq_<workload>_<prec>.json (round 1), read by bench.py for `valu_issue`.
 usage: python scripts/pmc_sq_summary.py COUNTERS.csv OUT.json"""
 import csv
 import json

@@ -1,4 +1,4 @@
-"""Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes into profiles/pmc_<workload>_<prec>.json (HBM bytes
+"""Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes into profiles/r01_final_pmc_<workload>_<prec>.json (round 1; bench.py now measures live) (HBM bytes
 per trace step: the sum over the listed kernels of each one's per-launch average), applying MI355X_MICROARCH.md's gfx950 correction: FETCH_SIZE reports 1/2 of the
 bytes of a wide coalesced read stream (x2), WRITE_SIZE is exact; both are in KiB.
 usage: python scripts/pmc_summary.py FETCH.csv WRITE.csv OUT.json [kernel-substring[,kernel-substring...]]"""
