@@ -13,8 +13,9 @@ recorded inside librt_hip.so on the stream the kernels run on.  At N=1 (unless -
 re-runs one frame of the same workload under rocprofv3 three times — FETCH_SIZE, WRITE_SIZE and eight
 SQ counters, each pass in its own process — so `roofline` (measured HBM bytes, bound "hbm") and
 `roofline_binding` (VALU issue slots and lane utilization, the resource that binds) are measured by
-this run, at this commit.  `cpu_baseline` times the CPU restatements on a bounded crop of the same
-workload on this host.
+this run, at this commit.  `cpu_baseline` times the reference's JS CPU path (oracle/js/pt_cpu.mjs, bit-exact to the
+reference's golden fixtures) under Node on this host at 1 thread and at the host's CPU share, plus
+the C port, each on a bounded crop of the same workload.
 """
 import argparse
 import ctypes as C
@@ -80,9 +81,51 @@ def make_tracer(cfg, precision, seed, device, accel="auto"):
     return rt
 
 
-def cpu_baseline(rt, cfg, side):
-    """Oracle (C restatement of the JS, 1 thread) on a centred side x side crop at full spp/depth."""
+# JS CPU baseline crops (side of the centred square crop, at full resolution, spp and depth): about
+# 10 s for one thread; the multi-thread run renders a crop twice the side
+JS_CROP = {"sample_scene": 64, "cornell": 48, "rtow": 32, "rtow4k": 24, "mesh50k": 4}
+
+
+def js_cpu_baseline(cfg_name, cfg, seed, workers, side):
+    """The reference's JS CPU path (oracle/js/pt_cpu.mjs, bit-exact to the reference on every golden
+    fixture) under Node on this host: `workers` worker_threads over row bands of a centred crop."""
+    import shutil
+    import subprocess
+    import tempfile
+    node = shutil.which("node")
+    if node is None:
+        return {"error": "node not found"}
+    w, h = cfg["w"], cfg["h"]
+    side = min(side, w, h)
+    x0, y0 = (w - side) // 2, (h - side) // 2
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+        json.dump(load_scene_json(cfg["scene"]), f)
+        path = f.name
+    try:
+        args = dict(scene=path, width=w, height=h, spp=cfg["spp"], depth=cfg["depth"], seed=seed,
+                    crop=[x0, y0, side, side], workers=workers)
+        r = subprocess.run([node, os.path.join(ROOT, "oracle", "js", "cpu_tool.mjs"), "bench", json.dumps(args)],
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            return {"error": r.stderr[-300:]}
+        out = json.loads(r.stdout)
+    finally:
+        os.unlink(path)
+    return {"value": round(out["msamples_per_s"], 6), "unit": "Msamples/s", "cores": out["workers"],
+            "nproc": out["nproc"], "kind": "js",
+            "sample": f"{side}x{side} crop at ({x0},{y0}) of the {w}x{h} frame, {cfg['spp']} spp, maxDepth "
+                      f"{cfg['depth']}: {out['samples']} samples in {out['render_s']:.1f} s (slowest worker; {out['wall_s']:.1f} s wall with worker start-up) (oracle/js/pt_cpu.mjs "
+                      f"under Node {out['node']}, {out['workers']} worker thread(s) over interleaved rows)"}
+
+
+def cpu_baseline(rt, cfg_name, cfg, seed, side):
+    """CPU baselines on this host: the JS CPU path at 1 thread (the reference's own model: one Node
+    event loop) and at the host's CPU share, plus the C port (oracle/pt_oracle.c, 1 thread)."""
     from oracle import binding
+    js_side = JS_CROP.get(cfg_name, 32)
+    one = js_cpu_baseline(cfg_name, cfg, seed, 1, js_side)
+    ncores = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS") or (os.cpu_count() or 1)))
+    many = js_cpu_baseline(cfg_name, cfg, seed, ncores, 2 * js_side)
     w, h = cfg["w"], cfg["h"]
     side = min(side, w, h)
     x0, y0 = (w - side) // 2, (h - side) // 2
@@ -92,9 +135,13 @@ def cpu_baseline(rt, cfg, side):
     binding.render(rt.packed(), st)
     dt = time.perf_counter() - t
     samples = side * side * st.samples
-    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
+    port = {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
             "sample": f"{side}x{side} crop at ({x0},{y0}) of the {w}x{h} frame, {st.samples} spp, "
                       f"maxDepth {cfg['depth']}: {samples} samples in {dt:.1f} s (oracle/pt_oracle.c, 1 thread)"}
+    res = dict(one) if "error" not in one else dict(port)
+    res["js_multi_core"] = many
+    res["c_port"] = port
+    return res
 
 
 # VALU issue ceiling: 256 CUs x 4 SIMD-32s, a wave64 VALU instruction holds its SIMD for 2 cycles (a
@@ -177,7 +224,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(rt, cfg, args.cpu_crop)
+        cpu = cpu_baseline(rt, args.config, cfg, args.seed, args.cpu_crop)
 
     job = ShardedRender(rt, rank=rank, world=world, device=torch.device("cuda", local))
     for _ in range(args.warmup):
