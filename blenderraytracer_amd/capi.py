@@ -9,7 +9,8 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "librt_hip.so")
 
-RT_ABI_VERSION = 1
+RT_ABI_VERSION = 2
+RT_MAX_DEVICES = 8
 
 # enums (include/rt_hip.h)
 RT_OBJ_SPHERE, RT_OBJ_PLANE, RT_OBJ_BOX, RT_OBJ_TRIANGLE, RT_OBJ_MESH = range(5)
@@ -55,7 +56,8 @@ class Settings(C.Structure):
                 ("seed", C.c_uint32), ("sample_begin", C.c_int32), ("sample_end", C.c_int32),
                 ("crop_x0", C.c_int32), ("crop_y0", C.c_int32), ("crop_w", C.c_int32), ("crop_h", C.c_int32),
                 ("precision", C.c_int32), ("batch_samples", C.c_int32), ("denoise", C.c_int32),
-                ("denoise_weights", C.c_double * 2), ("accel", C.c_int32), ("_pad", C.c_int32)]
+                ("denoise_weights", C.c_double * 2), ("accel", C.c_int32), ("device_count", C.c_int32),
+                ("devices", C.c_int32 * 8), ("_pad2", C.c_int32)]
 
 
 class Output(C.Structure):

@@ -51,6 +51,24 @@ double get_num(napi_env env, napi_value obj, const char* key, double dflt) {
     return d;
 }
 
+// Up to `max` numbers of an Array property (e.g. settings.devices); returns how many were read.
+int get_int_array(napi_env env, napi_value obj, const char* key, int32_t* out, int max) {
+    napi_value v;
+    if (!get_prop(env, obj, key, &v)) return 0;
+    bool is = false;
+    if (napi_is_array(env, v, &is) != napi_ok || !is) return 0;
+    uint32_t len = 0;
+    napi_get_array_length(env, v, &len);
+    int n = 0;
+    for (uint32_t i = 0; i < len && n < max; ++i) {
+        napi_value e;
+        double d = 0;
+        if (napi_get_element(env, v, i, &e) != napi_ok || napi_get_value_double(env, e, &d) != napi_ok) return -1;
+        out[n++] = (int32_t)d;
+    }
+    return len > (uint32_t)max ? -1 : n;
+}
+
 // Raw bytes of a TypedArray / ArrayBuffer / DataView property.
 bool get_bytes(napi_env env, napi_value obj, const char* key, void** data, size_t* bytes) {
     napi_value v;
@@ -307,6 +325,13 @@ napi_value render(napi_env env, napi_callback_info info) {
     st.accel = (int32_t)get_num(env, s, "accel", RT_ACCEL_AUTO);
     st.denoise_weights[0] = get_num(env, s, "denoiseW1", 0.0);
     st.denoise_weights[1] = get_num(env, s, "denoiseW2", 0.0);
+    // settings.devices: [ordinals] -> rt_settings.device_count / devices (multi-GPU sample split)
+    const int nd = get_int_array(env, s, "devices", st.devices, RT_MAX_DEVICES);
+    if (nd < 0) {
+        delete job;
+        return throw_err(env, "render: settings.devices must be an Array of at most 8 device ordinals");
+    }
+    st.device_count = nd;
     job->want_mean = get_num(env, s, "wantMean", 0) != 0;
     job->want_counts = get_num(env, s, "wantCounts", 0) != 0;
     const int cw = st.crop_w > 0 ? st.crop_w : st.width, ch = st.crop_h > 0 ? st.crop_h : st.height;

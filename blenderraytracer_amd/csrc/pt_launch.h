@@ -36,6 +36,10 @@ bool trace_uses_pool();
 // tiles x kPartialBytesPerTile) launch_trace splits the samples over several launches.
 size_t pool_partial_bytes(int cw, int ch, int ns, bool tri_bvh);
 
+// dst[i] += src[i] (n elements, both on the stream's device): merging the shards of a multi-device render
+template <class T>
+hipError_t launch_add(T* dst, const T* src, size_t n, hipStream_t stream);
+
 struct FinalizeParams {
     int n;
     int samples;

@@ -274,12 +274,14 @@ bool trace_uses_pool() {
     return v == 1;
 }
 
-// Samples per pool wave: ~1.5 sqrt(ns) (0.75 sqrt(ns) when the scene has a triangle BVH: its walks
+// Samples per pool wave: ~4 sqrt(ns) (0.75 sqrt(ns) when the scene has a triangle BVH: its walks
 // vary more in length, so shorter waves pay), halved (>= 4) until the launch has >= 64k waves (4x the
 // chip's 16k wave slots).  Short waves shorten the frame's drain tail; long ones shorten each wave's
-// own tail (its last items finish at different times) and write fewer chunk partials.  Measured best
-// chunks, 1080p: RTOW 512 spp 24-34, 64 spp 16; mesh50k 256 spp 12, 32 spp 8; Cornell 512^2 x 64 spp
-// (4096 tiles) 4.  RT_POOL_CHUNK overrides (A/B runs).
+// own tail (its last items finish at different times) and write fewer chunk partials (each chunk is
+// 24 B per pixel written and read back once).  Measured (LDS-accumulating pool, 1080p): RTOW 512 spp
+// c34 / c48 / c64 / c96 within 0.6 % (c90: 6 chunks, 0.6 GB of partials per frame instead of 1.6);
+// mesh50k 256 spp c12 / c16 / c24 / c32 6786 / 6673 / 6687 / 6391; Cornell 512^2 x 64 spp (4096
+// tiles) 4.  RT_POOL_CHUNK overrides (A/B runs).
 static int pool_chunk(int ns, int tiles, bool tri_bvh) {
     static int v = -1;
     if (v == -1) {
@@ -287,7 +289,7 @@ static int pool_chunk(int ns, int tiles, bool tri_bvh) {
         v = e ? std::max(1, atoi(e)) : 0;
     }
     if (v) return v;
-    int c = std::min(64, std::max(4, (int)((tri_bvh ? 0.75 : 1.5) * std::sqrt((double)ns) + 0.5)));
+    int c = std::min(128, std::max(4, (int)((tri_bvh ? 0.75 : 4.0) * std::sqrt((double)ns) + 0.5)));
     while (c > 4 && (long long)tiles * ((ns + c - 1) / c) < 65536) c = std::max(4, c / 2);
     return c;
 }
@@ -376,6 +378,22 @@ hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Cou
 
 template hipError_t launch_trace<double>(const SceneView<double>&, const ImageParams&, const Counters&, bool, hipStream_t);
 template hipError_t launch_trace<float>(const SceneView<float>&, const ImageParams&, const Counters&, bool, hipStream_t);
+
+// ---- multi-device sample split: dst += src elementwise (the shards' sums / counters, in shard order) ----
+template <class T>
+__global__ __launch_bounds__(256) void add_kernel(T* __restrict__ dst, const T* __restrict__ src, const size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] += src[i];
+}
+
+template <class T>
+hipError_t launch_add(T* dst, const T* src, size_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(add_kernel<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dst, src, n);
+    return hipGetLastError();
+}
+template hipError_t launch_add<double>(double*, const double*, size_t, hipStream_t);
+template hipError_t launch_add<uint32_t>(uint32_t*, const uint32_t*, size_t, hipStream_t);
 
 // ---- epilogue: mean, toneMap, gammaCorrect, RGBA8 (ray-tracer.js:208-252, post-processor.js:9-42) ----
 __device__ __forceinline__ uint8_t to_u8(double c) {

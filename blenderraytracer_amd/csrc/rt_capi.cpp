@@ -139,31 +139,84 @@ double now_ms() {
     return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
 }
 
-}  // namespace
-
-struct rt_scene {
+// Everything one device holds for a scene: the scene arrays in its HBM, a stream, the running sums
+// and counters of the samples it traces, the pool's chunk partials and the work totals (scratch).
+struct DeviceState {
     int device = 0;
     DeviceScene<double> s64;
     DeviceScene<float> s32;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[2] = {};             // trace timing
+    DevBuf<double> sum;
+    DevBuf<uint32_t> segs, draws;
+    DevBuf<unsigned long long> total;
+    DevBuf<double> part;               // sample-pool chunk partials (ensure_partials)
+    hipEvent_t scratch_ev = nullptr;   // recorded after every use of part / total (order_scratch)
+    hipStream_t scratch_stream = nullptr;
+    bool scratch_used = false;
+
+    int init(int dev, const HostScene& hs, const rt_scene_desc& d) {
+        device = dev;
+        hipError_t e = hipSetDevice(dev);
+        if (e != hipSuccess) return fail(RT_ERR_DEVICE, "hipSetDevice(%d): %s", dev, hipGetErrorString(e));
+        int rc;
+        if ((rc = build_device(s64, hs, d)) || (rc = build_device(s32, hs, d))) return rc;
+        e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+        for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreate(&ev[k]);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&scratch_ev, hipEventDisableTiming);
+        if (e != hipSuccess) return fail(RT_ERR_DEVICE, "stream/event create: %s", hipGetErrorString(e));
+        return RT_OK;
+    }
+    void release() {
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        s64.release();
+        s32.release();
+        sum.release(); segs.release(); draws.release(); total.release(); part.release();
+        for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (scratch_ev) (void)hipEventDestroy(scratch_ev);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+// A deep copy of the scene descriptor, so replicas can be uploaded to more devices later.
+struct DescCopy {
+    rt_scene_desc d{};
+    std::vector<rt_object_desc> objects;
+    std::vector<rt_material_desc> materials;
+    std::vector<double> triangles;
+    void set(const rt_scene_desc& src) {
+        d = src;
+        objects.assign(src.objects, src.objects + std::max(0, src.num_objects));
+        materials.assign(src.materials, src.materials + std::max(0, src.num_materials));
+        triangles.assign(src.triangles, src.triangles + 12 * (size_t)std::max(0, src.num_triangles));
+        d.objects = objects.data();
+        d.materials = materials.data();
+        d.triangles = triangles.data();
+    }
+};
+
+}  // namespace
+
+struct rt_scene {
+    DeviceState home;               // the device of rt_scene_create: epilogue, outputs, checkpoint
+    std::vector<DeviceState*> replicas;   // rt_settings.devices[k] for k >= 1 (created on first use)
+    HostScene hs;
+    DescCopy desc;
     int num_prims = 0;
     int bvh_prims = 0;              // spheres + triangles (the primitives the BVHs cover)
     bool bvh_ok = true;             // both trees fit the traversal stack (depth <= RT_BVH_STACK)
     bool tri_bvh = false;           // the scene has a triangle BVH (pool chunk choice)
     double record_bytes = 0;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev[4] = {};
-    DevBuf<double> sum, mean;
+    hipEvent_t ev[2] = {};          // epilogue timing
+    DevBuf<double> mean, stage;     // stage: a shard's sums copied from its device
+    DevBuf<uint32_t> stage_u;
     DevBuf<float> post, post_raw;   // post_raw: pre-denoise floatData
     DevBuf<uint8_t> rgba;
-    DevBuf<uint32_t> segs, draws;
-    DevBuf<unsigned long long> total;
-    DevBuf<double> part;            // sample-pool chunk partials (ensure_partials)
-    hipEvent_t scratch_ev = nullptr;   // recorded after every use of part / total (order_scratch)
-    hipStream_t scratch_stream = nullptr;
-    bool scratch_used = false;
     std::atomic<int> cancel{0};
     size_t ckpt_pixels = 0;         // progressive state of the last rt_render / rt_render_resume:
-    int ckpt_done = 0;              // `sum` holds samples [sample_begin, ckpt_done) of ckpt_pixels pixels
+    int ckpt_done = 0;              // `home.sum` holds samples [sample_begin, ckpt_done) of ckpt_pixels pixels
 };
 
 namespace {
@@ -183,6 +236,14 @@ int check_settings(const rt_settings* s, int* cw, int* ch) {
     if (s->accel < RT_ACCEL_AUTO || s->accel > RT_ACCEL_BVH) return fail(RT_ERR_INVALID, "accel %d", s->accel);
     if (s->denoise && (*cw != s->width || *ch != s->height))
         return fail(RT_ERR_INVALID, "denoise needs the full frame (PostProcessor.denoise clamps to the image edge)");
+    if (s->device_count < 0 || s->device_count > RT_MAX_DEVICES)
+        return fail(RT_ERR_INVALID, "device_count %d (at most %d)", s->device_count, RT_MAX_DEVICES);
+    if (s->device_count > 1) {
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RT_ERR_NO_DEVICE, "no HIP device visible");
+        for (int k = 0; k < s->device_count; ++k)
+            if (s->devices[k] < 0 || s->devices[k] >= ndev) return fail(RT_ERR_INVALID, "devices[%d] = %d of %d", k, s->devices[k], ndev);
+    }
     return RT_OK;
 }
 
@@ -226,18 +287,19 @@ int check_accel(const rt_scene* sc, const rt_settings* s) {
     return RT_OK;
 }
 
-hipError_t trace(rt_scene* sc, const rt_settings* s, const ImageParams& im, const Counters& c, hipStream_t st) {
+hipError_t trace(const rt_scene* sc, const DeviceState& ds, const rt_settings* s, const ImageParams& im,
+                 const Counters& c, hipStream_t st) {
     if (im.max_depth <= 0) return hipSuccess;   // rayColor(ray, depth<=0) is 0: nothing to trace
     const bool bvh = use_bvh(sc, s);
-    if (s->precision == RT_PREC_F32) return launch_trace<float>(sc->s32.view, im, c, bvh, st);
-    return launch_trace<double>(sc->s64.view, im, c, bvh, st);
+    if (s->precision == RT_PREC_F32) return launch_trace<float>(ds.s32.view, im, c, bvh, st);
+    return launch_trace<double>(ds.s64.view, im, c, bvh, st);
 }
 
 // Sample-pool chunk partials (pool_partial_bytes, pt_trace.hip): all of a launch's chunks when they fit
 // the budget (RT_PART_MB, default 2 GiB, at most 10 % of the free device memory), else as many
 // chunks as fit (launch_trace then splits the samples over several launches).  RTOW 1080p x 512 spp
-// needs 0.8 GB; a launch with a single chunk needs none.  Kept by the scene between renders.
-int ensure_partials(rt_scene* sc, const rt_settings* s, int cw, int ch, int samples, Counters& c) {
+// needs 0.3 GB; a launch with a single chunk needs none.  Kept by the device state between renders.
+int ensure_partials(const rt_scene* sc, DeviceState& ds, int cw, int ch, int samples, Counters& c) {
     if (!trace_uses_pool() || samples <= 0 || cw <= 0 || ch <= 0) return RT_OK;
     const size_t want_all = pool_partial_bytes(cw, ch, samples, sc->tri_bvh);
     if (want_all == 0) return RT_OK;
@@ -248,34 +310,34 @@ int ensure_partials(rt_scene* sc, const rt_settings* s, int cw, int ch, int samp
         budget = (size_t)(e ? std::max(1LL, atoll(e)) : 2048LL) << 20;
     }
     size_t want = want_all;
-    if (want > sc->part.n * sizeof(double)) {
+    if (want > ds.part.n * sizeof(double)) {
         size_t free_b = 0, total_b = 0, cap = budget;
-        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = std::min(cap, (free_b + sc->part.n * sizeof(double)) / 10);
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = std::min(cap, (free_b + ds.part.n * sizeof(double)) / 10);
         want = std::min(want, std::max<size_t>(cap / per_chunk, 1) * per_chunk);
-        while (want > sc->part.n * sizeof(double)) {
-            if (sc->part.ensure(want / sizeof(double)) == hipSuccess) break;
+        while (want > ds.part.n * sizeof(double)) {
+            if (ds.part.ensure(want / sizeof(double)) == hipSuccess) break;
             (void)hipGetLastError();
             if (want == per_chunk) return fail(RT_ERR_DEVICE, "sample pool: cannot allocate %zu bytes", per_chunk);
             want = std::max<size_t>(want / per_chunk / 2, 1) * per_chunk;
         }
     }
-    c.part = sc->part.p;
-    c.part_bytes = sc->part.n * sizeof(double);
+    c.part = ds.part.p;
+    c.part_bytes = ds.part.n * sizeof(double);
     return RT_OK;
 }
 
-// The scene's scratch buffers (chunk partials, work totals) are shared by every call on the scene.
-// A call on stream `st` first waits for the previous user of the scratch (possibly another stream:
+// A device state's scratch buffers (chunk partials, work totals) are shared by every call on it.  A
+// call on stream `st` first waits for the previous user of the scratch (possibly another stream:
 // rt_trace_device on a caller's stream, rt_render on the scene's own) and records the event again
 // when it has enqueued its last use, so asynchronous calls on different streams never overlap on it.
-hipError_t order_scratch(rt_scene* sc, hipStream_t st) {
-    if (!sc->scratch_used || sc->scratch_stream == st) return hipSuccess;
-    return hipStreamWaitEvent(st, sc->scratch_ev, 0);
+hipError_t order_scratch(DeviceState& ds, hipStream_t st) {
+    if (!ds.scratch_used || ds.scratch_stream == st) return hipSuccess;
+    return hipStreamWaitEvent(st, ds.scratch_ev, 0);
 }
-hipError_t release_scratch(rt_scene* sc, hipStream_t st) {
-    sc->scratch_stream = st;
-    sc->scratch_used = true;
-    return hipEventRecord(sc->scratch_ev, st);
+hipError_t release_scratch(DeviceState& ds, hipStream_t st) {
+    ds.scratch_stream = st;
+    ds.scratch_used = true;
+    return hipEventRecord(ds.scratch_ev, st);
 }
 
 // totals = [segments, BVH nodes, sphere tests, triangle tests] of the launches
@@ -284,7 +346,7 @@ void fill_stats(rt_stats* st, const rt_scene* sc, const rt_settings* s, const un
     st->samples = (uint64_t)n * (uint64_t)std::max(0, im.s_end - im.s_begin);
     st->segments = totals[0];
     if (use_bvh(sc, s)) {
-        const uint64_t brute = (uint64_t)sc->s64.view.num_planes + sc->s64.view.num_boxes;
+        const uint64_t brute = (uint64_t)sc->home.s64.view.num_planes + sc->home.s64.view.num_boxes;
         st->node_visits = totals[1];
         st->sphere_tests = totals[2];
         st->tri_tests = totals[3];
@@ -296,6 +358,44 @@ void fill_stats(rt_stats* st, const rt_scene* sc, const rt_settings* s, const un
         st->prim_tests = totals[0] * (uint64_t)sc->num_prims;
         st->algorithmic_bytes = (double)totals[0] * sc->record_bytes + 12.0 * (double)n;
     }
+}
+
+// The device states of a render: shard k of rt_settings.devices (k = 0: the scene's own device when
+// it is listed first, else a replica), created and uploaded on first use.
+int shard_states(rt_scene* sc, const rt_settings* s, std::vector<DeviceState*>& out) {
+    out.clear();
+    const int n = s->device_count > 1 ? s->device_count : 1;
+    if (n == 1) {
+        out.push_back(&sc->home);
+        return RT_OK;
+    }
+    for (int k = 0; k < n; ++k) {
+        const int dev = s->devices[k];
+        if (k == 0 && dev == sc->home.device) {
+            out.push_back(&sc->home);
+            continue;
+        }
+        const size_t slot = (size_t)k;                     // replica of shard k
+        if (sc->replicas.size() <= slot) sc->replicas.resize(slot + 1, nullptr);
+        DeviceState*& r = sc->replicas[slot];
+        if (r && r->device != dev) {                       // the device list changed: re-create
+            r->release();
+            delete r;
+            r = nullptr;
+        }
+        if (!r) {
+            r = new DeviceState();
+            const int rc = r->init(dev, sc->hs, sc->desc.d);
+            if (rc) {
+                r->release();
+                delete r;
+                r = nullptr;
+                return rc;
+            }
+        }
+        out.push_back(r);
+    }
+    return RT_OK;
 }
 
 }  // namespace
@@ -334,29 +434,26 @@ int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RT_ERR_NO_DEVICE, "no HIP device visible");
     if (device < 0 || device >= ndev) return fail(RT_ERR_INVALID, "device %d of %d", device, ndev);
-    HostScene hs;
-    std::string err;
-    if (!pack_host(*desc, hs, err)) return fail(RT_ERR_INVALID, "%s", err.c_str());
-    build_bvhs(hs);
-    int rc;
-    HIP_TRY(hipSetDevice(device));
     rt_scene* sc = new rt_scene();
-    sc->device = device;
-    sc->num_prims = hs.num_prims;
-    sc->bvh_prims = (int)(hs.sphere_r.size() + hs.tri_mat.size());
-    sc->bvh_ok = hs.bvh_depth <= RT_BVH_STACK;
-    sc->tri_bvh = !hs.tri_wide.empty();
-    sc->record_bytes = hs.record_bytes;
-    if ((rc = build_device(sc->s64, hs, *desc)) || (rc = build_device(sc->s32, hs, *desc))) {
+    std::string err;
+    if (!pack_host(*desc, sc->hs, err)) {
+        delete sc;
+        return fail(RT_ERR_INVALID, "%s", err.c_str());
+    }
+    build_bvhs(sc->hs);
+    sc->desc.set(*desc);
+    sc->num_prims = sc->hs.num_prims;
+    sc->bvh_prims = (int)(sc->hs.sphere_r.size() + sc->hs.tri_mat.size());
+    sc->bvh_ok = sc->hs.bvh_depth <= RT_BVH_STACK;
+    sc->tri_bvh = !sc->hs.tri_wide.empty();
+    sc->record_bytes = sc->hs.record_bytes;
+    int rc = sc->home.init(device, sc->hs, sc->desc.d);
+    hipError_t e = hipSuccess;
+    for (int k = 0; k < 2 && !rc && e == hipSuccess; ++k) e = hipEventCreate(&sc->ev[k]);
+    if (!rc && e != hipSuccess) rc = fail(RT_ERR_DEVICE, "event create: %s", hipGetErrorString(e));
+    if (rc) {
         rt_scene_destroy(sc);
         return rc;
-    }
-    hipError_t e = hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking);
-    for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreate(&sc->ev[k]);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&sc->scratch_ev, hipEventDisableTiming);
-    if (e != hipSuccess) {
-        rt_scene_destroy(sc);
-        return fail(RT_ERR_DEVICE, "stream/event create: %s", hipGetErrorString(e));
     }
     *out = sc;
     return RT_OK;
@@ -364,16 +461,17 @@ int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out) {
 
 void rt_scene_destroy(rt_scene* sc) {
     if (!sc) return;
-    (void)hipSetDevice(sc->device);
-    if (sc->stream) (void)hipStreamSynchronize(sc->stream);
-    sc->s64.release();
-    sc->s32.release();
-    sc->sum.release(); sc->mean.release(); sc->post.release(); sc->post_raw.release(); sc->rgba.release();
-    sc->segs.release(); sc->draws.release(); sc->total.release(); sc->part.release();
-    if (sc->scratch_ev) (void)hipEventDestroy(sc->scratch_ev);
+    for (DeviceState* r : sc->replicas)
+        if (r) {
+            r->release();
+            delete r;
+        }
+    sc->home.release();
+    (void)hipSetDevice(sc->home.device);
+    sc->mean.release(); sc->stage.release(); sc->stage_u.release(); sc->post.release(); sc->post_raw.release();
+    sc->rgba.release();
     for (auto& e : sc->ev)
         if (e) (void)hipEventDestroy(e);
-    if (sc->stream) (void)hipStreamDestroy(sc->stream);
     delete sc;
 }
 
@@ -387,6 +485,44 @@ int rt_cancel(rt_scene* sc) {
 
 namespace {
 
+// Shard k of the sample range [b, e) over n shards (contiguous, sizes differ by at most one).
+void shard_range(int b, int e, int k, int n, int& sb, int& se) {
+    const long long len = e - b;
+    sb = b + (int)(len * k / n);
+    se = b + (int)(len * (k + 1) / n);
+}
+
+// Adds the replicas' sums (and counters) of the batch just traced into the home device's, in shard
+// order (peer copies over xGMI into a staging buffer on the home device, then dst += stage), and zeroes
+// the replicas' buffers for the next batch.  Merging after every batch keeps the running sums on the
+// home device exactly what a checkpoint saves, so a resumed render is bit-identical.
+int merge_shards(rt_scene* sc, const std::vector<DeviceState*>& states, size_t n, bool segs, bool draws) {
+    DeviceState& h = sc->home;
+    for (DeviceState* ds : states) {
+        if (ds == &h) continue;
+        HIP_TRY(hipSetDevice(ds->device));
+        HIP_TRY(hipStreamSynchronize(ds->stream));
+        HIP_TRY(hipSetDevice(h.device));
+        HIP_TRY(sc->stage.ensure(3 * n));
+        HIP_TRY(hipMemcpyPeerAsync(sc->stage.p, h.device, ds->sum.p, ds->device, 3 * n * sizeof(double), h.stream));
+        HIP_TRY(launch_add<double>(h.sum.p, sc->stage.p, 3 * n, h.stream));
+        for (int k = 0; k < 2; ++k) {
+            if (!(k == 0 ? segs : draws)) continue;
+            HIP_TRY(sc->stage_u.ensure(n));
+            HIP_TRY(hipMemcpyPeerAsync(sc->stage_u.p, h.device, (k == 0 ? ds->segs : ds->draws).p, ds->device,
+                                       n * sizeof(uint32_t), h.stream));
+            HIP_TRY(launch_add<uint32_t>((k == 0 ? h.segs : h.draws).p, sc->stage_u.p, n, h.stream));
+        }
+        HIP_TRY(hipStreamSynchronize(h.stream));     // the staging buffers are reused by the next shard
+        HIP_TRY(hipSetDevice(ds->device));
+        HIP_TRY(hipMemsetAsync(ds->sum.p, 0, 3 * n * sizeof(double), ds->stream));
+        if (segs) HIP_TRY(hipMemsetAsync(ds->segs.p, 0, n * sizeof(uint32_t), ds->stream));
+        if (draws) HIP_TRY(hipMemsetAsync(ds->draws.p, 0, n * sizeof(uint32_t), ds->stream));
+        HIP_TRY(hipSetDevice(h.device));
+    }
+    return RT_OK;
+}
+
 // rt_render and rt_render_resume: trace samples [first, sample_end) on top of `sums_in` (NULL: zeros)
 int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progress_fn progress, void* user,
                 rt_stats* stats, const double* sums_in, int first) {
@@ -396,72 +532,123 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     int rc = check_settings(s, &cw, &ch);
     if (!rc) rc = check_accel(sc, s);
     if (rc) return rc;
-    HIP_TRY(hipSetDevice(sc->device));
+    std::vector<DeviceState*> states;
+    if ((rc = shard_states(sc, s, states))) return rc;
     sc->cancel.store(0);
     const size_t n = (size_t)cw * ch;
     const bool want_segs = out && out->segments, want_draws = out && out->draws;
-    HIP_TRY(sc->sum.ensure(3 * n));
-    HIP_TRY(sc->total.ensure(kTotalSlots));
-    HIP_TRY(order_scratch(sc, sc->stream));
-    if (sums_in) HIP_TRY(hipMemcpyAsync(sc->sum.p, sums_in, 3 * n * sizeof(double), hipMemcpyHostToDevice, sc->stream));
-    else HIP_TRY(hipMemsetAsync(sc->sum.p, 0, 3 * n * sizeof(double), sc->stream));
-    HIP_TRY(hipMemsetAsync(sc->total.p, 0, kTotalSlots * sizeof(unsigned long long), sc->stream));
-    Counters c{sc->sum.p, nullptr, nullptr, sc->total.p};
-    if (want_segs) {
-        HIP_TRY(sc->segs.ensure(n));
-        HIP_TRY(hipMemsetAsync(sc->segs.p, 0, n * sizeof(uint32_t), sc->stream));
-        c.segs = sc->segs.p;
-    }
-    if (want_draws) {
-        HIP_TRY(sc->draws.ensure(n));
-        HIP_TRY(hipMemsetAsync(sc->draws.p, 0, n * sizeof(uint32_t), sc->stream));
-        c.draws = sc->draws.p;
-    }
     ImageParams im = image_params(s, cw, ch);
     im.s_begin = std::max(im.s_begin, first);
     const int s0 = im.s_begin, s1 = std::max(im.s_end, s0);
     const int batch = s->batch_samples > 0 ? s->batch_samples : std::max(1, s1 - s0);
-    if (s->max_depth > 0 && (rc = ensure_partials(sc, s, cw, ch, std::min(batch, s1 - s0), c))) return rc;
+    const int nsh = (int)states.size();
+    std::vector<Counters> cs(nsh);
+    for (int k = 0; k < nsh; ++k) {
+        DeviceState& ds = *states[k];
+        HIP_TRY(hipSetDevice(ds.device));
+        HIP_TRY(ds.sum.ensure(3 * n));
+        HIP_TRY(ds.total.ensure(kTotalSlots));
+        HIP_TRY(order_scratch(ds, ds.stream));
+        if (sums_in && &ds == &sc->home)
+            HIP_TRY(hipMemcpyAsync(ds.sum.p, sums_in, 3 * n * sizeof(double), hipMemcpyHostToDevice, ds.stream));
+        else
+            HIP_TRY(hipMemsetAsync(ds.sum.p, 0, 3 * n * sizeof(double), ds.stream));
+        HIP_TRY(hipMemsetAsync(ds.total.p, 0, kTotalSlots * sizeof(unsigned long long), ds.stream));
+        Counters& c = cs[k];
+        c = Counters{ds.sum.p, nullptr, nullptr, ds.total.p};
+        if (want_segs) {
+            HIP_TRY(ds.segs.ensure(n));
+            HIP_TRY(hipMemsetAsync(ds.segs.p, 0, n * sizeof(uint32_t), ds.stream));
+            c.segs = ds.segs.p;
+        }
+        if (want_draws) {
+            HIP_TRY(ds.draws.ensure(n));
+            HIP_TRY(hipMemsetAsync(ds.draws.p, 0, n * sizeof(uint32_t), ds.stream));
+            c.draws = ds.draws.p;
+        }
+        int b0, b1;
+        shard_range(s0, s0 + std::min(batch, s1 - s0), k, nsh, b0, b1);
+        if (s->max_depth > 0 && (rc = ensure_partials(sc, ds, cw, ch, std::max(1, b1 - b0), c))) return rc;
+    }
+    if (states[0] != &sc->home) {                 // the home device only merges: its buffers start here
+        DeviceState& h = sc->home;
+        HIP_TRY(hipSetDevice(h.device));
+        HIP_TRY(h.sum.ensure(3 * n));
+        if (sums_in) HIP_TRY(hipMemcpyAsync(h.sum.p, sums_in, 3 * n * sizeof(double), hipMemcpyHostToDevice, h.stream));
+        else HIP_TRY(hipMemsetAsync(h.sum.p, 0, 3 * n * sizeof(double), h.stream));
+        if (want_segs) {
+            HIP_TRY(h.segs.ensure(n));
+            HIP_TRY(hipMemsetAsync(h.segs.p, 0, n * sizeof(uint32_t), h.stream));
+        }
+        if (want_draws) {
+            HIP_TRY(h.draws.ensure(n));
+            HIP_TRY(hipMemsetAsync(h.draws.p, 0, n * sizeof(uint32_t), h.stream));
+        }
+    }
     sc->ckpt_pixels = n;
     sc->ckpt_done = s0;
     double kernel_ms = 0;
+    int status = RT_OK;
     for (int b = s0; b < s1; b += batch) {
-        ImageParams bi = im;
-        bi.s_begin = b;
-        bi.s_end = std::min(s1, b + batch);
-        HIP_TRY(hipEventRecord(sc->ev[0], sc->stream));
-        HIP_TRY(trace(sc, s, bi, c, sc->stream));
-        HIP_TRY(hipEventRecord(sc->ev[1], sc->stream));
-        HIP_TRY(hipEventSynchronize(sc->ev[1]));
-        float ms = 0;
-        HIP_TRY(hipEventElapsedTime(&ms, sc->ev[0], sc->ev[1]));
-        kernel_ms += ms;
-        sc->ckpt_done = bi.s_end;
-        if (progress && bi.s_end < s1) {
-            if (progress((double)(bi.s_end - s0) / (double)(s1 - s0), user)) sc->cancel.store(1);
+        const int be = std::min(s1, b + batch);
+        for (int k = 0; k < nsh; ++k) {           // every shard's launches first: the devices run together
+            DeviceState& ds = *states[k];
+            ImageParams bi = im;
+            shard_range(b, be, k, nsh, bi.s_begin, bi.s_end);
+            HIP_TRY(hipSetDevice(ds.device));
+            HIP_TRY(hipEventRecord(ds.ev[0], ds.stream));
+            HIP_TRY(trace(sc, ds, s, bi, cs[k], ds.stream));
+            HIP_TRY(hipEventRecord(ds.ev[1], ds.stream));
         }
-        if (sc->cancel.load()) return fail(RT_ERR_CANCELLED, "render cancelled after %d samples", bi.s_end);
+        float batch_ms = 0;
+        for (int k = 0; k < nsh; ++k) {
+            DeviceState& ds = *states[k];
+            HIP_TRY(hipSetDevice(ds.device));
+            HIP_TRY(hipEventSynchronize(ds.ev[1]));
+            float ms = 0;
+            HIP_TRY(hipEventElapsedTime(&ms, ds.ev[0], ds.ev[1]));
+            batch_ms = std::max(batch_ms, ms);
+        }
+        kernel_ms += batch_ms;
+        if (nsh > 1 && (rc = merge_shards(sc, states, n, want_segs, want_draws))) return rc;
+        sc->ckpt_done = be;
+        if (progress && be < s1) {
+            if (progress((double)(be - s0) / (double)(s1 - s0), user)) sc->cancel.store(1);
+        }
+        if (sc->cancel.load()) {
+            status = fail(RT_ERR_CANCELLED, "render cancelled after %d samples", be);
+            break;
+        }
     }
+    unsigned long long totals[kTotalSlots] = {};
+    for (DeviceState* ds : states) {
+        unsigned long long t[kTotalSlots] = {};
+        HIP_TRY(hipSetDevice(ds->device));
+        HIP_TRY(hipMemcpyAsync(t, ds->total.p, sizeof t, hipMemcpyDeviceToHost, ds->stream));
+        HIP_TRY(release_scratch(*ds, ds->stream));
+        HIP_TRY(hipStreamSynchronize(ds->stream));
+        for (int k = 0; k < kTotalSlots; ++k) totals[k] += t[k];
+    }
+    if (status != RT_OK) return status;
+    DeviceState& h = sc->home;
+    HIP_TRY(hipSetDevice(h.device));
     const bool want_mean = out && out->mean, want_post = out && out->post, want_rgba = out && out->rgba8;
     if (want_mean) HIP_TRY(sc->mean.ensure(3 * n));
     if (want_post) HIP_TRY(sc->post.ensure(4 * n));
     if (want_rgba) HIP_TRY(sc->rgba.ensure(4 * n));
-    HIP_TRY(hipEventRecord(sc->ev[2], sc->stream));
-    HIP_TRY(epilogue(sc, s, cw, ch, sc->sum.p, want_mean ? sc->mean.p : nullptr, want_post ? sc->post.p : nullptr,
-                     want_rgba ? sc->rgba.p : nullptr, sc->stream));
-    HIP_TRY(hipEventRecord(sc->ev[3], sc->stream));
-    if (want_mean) HIP_TRY(hipMemcpyAsync(out->mean, sc->mean.p, 3 * n * sizeof(double), hipMemcpyDeviceToHost, sc->stream));
-    if (want_post) HIP_TRY(hipMemcpyAsync(out->post, sc->post.p, 4 * n * sizeof(float), hipMemcpyDeviceToHost, sc->stream));
-    if (want_rgba) HIP_TRY(hipMemcpyAsync(out->rgba8, sc->rgba.p, 4 * n, hipMemcpyDeviceToHost, sc->stream));
-    if (want_segs) HIP_TRY(hipMemcpyAsync(out->segments, sc->segs.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, sc->stream));
-    if (want_draws) HIP_TRY(hipMemcpyAsync(out->draws, sc->draws.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, sc->stream));
-    unsigned long long totals[kTotalSlots] = {};
-    HIP_TRY(hipMemcpyAsync(totals, sc->total.p, sizeof totals, hipMemcpyDeviceToHost, sc->stream));
-    HIP_TRY(release_scratch(sc, sc->stream));
-    HIP_TRY(hipStreamSynchronize(sc->stream));
+    HIP_TRY(hipEventRecord(sc->ev[0], h.stream));
+    HIP_TRY(epilogue(sc, s, cw, ch, h.sum.p, want_mean ? sc->mean.p : nullptr, want_post ? sc->post.p : nullptr,
+                     want_rgba ? sc->rgba.p : nullptr, h.stream));
+    HIP_TRY(hipEventRecord(sc->ev[1], h.stream));
+    if (want_mean) HIP_TRY(hipMemcpyAsync(out->mean, sc->mean.p, 3 * n * sizeof(double), hipMemcpyDeviceToHost, h.stream));
+    if (want_post) HIP_TRY(hipMemcpyAsync(out->post, sc->post.p, 4 * n * sizeof(float), hipMemcpyDeviceToHost, h.stream));
+    if (want_rgba) HIP_TRY(hipMemcpyAsync(out->rgba8, sc->rgba.p, 4 * n, hipMemcpyDeviceToHost, h.stream));
+    if (want_segs) HIP_TRY(hipMemcpyAsync(out->segments, h.segs.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, h.stream));
+    if (want_draws) HIP_TRY(hipMemcpyAsync(out->draws, h.draws.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, h.stream));
+    HIP_TRY(hipStreamSynchronize(h.stream));
     if (stats) {
         float fms = 0;
-        HIP_TRY(hipEventElapsedTime(&fms, sc->ev[2], sc->ev[3]));
+        HIP_TRY(hipEventElapsedTime(&fms, sc->ev[0], sc->ev[1]));
         stats->kernel_ms = kernel_ms;
         stats->finalize_ms = fms;
         fill_stats(stats, sc, s, totals, n, im);
@@ -492,9 +679,9 @@ int rt_render_checkpoint(rt_scene* sc, double* sums, size_t count, int32_t* samp
     if (sc->ckpt_pixels == 0) return fail(RT_ERR_INVALID, "no render to checkpoint");
     if (count != 3 * sc->ckpt_pixels)
         return fail(RT_ERR_INVALID, "checkpoint holds %zu doubles, caller gave %zu", 3 * sc->ckpt_pixels, count);
-    HIP_TRY(hipSetDevice(sc->device));
-    HIP_TRY(hipMemcpyAsync(sums, sc->sum.p, count * sizeof(double), hipMemcpyDeviceToHost, sc->stream));
-    HIP_TRY(hipStreamSynchronize(sc->stream));
+    HIP_TRY(hipSetDevice(sc->home.device));
+    HIP_TRY(hipMemcpyAsync(sums, sc->home.sum.p, count * sizeof(double), hipMemcpyDeviceToHost, sc->home.stream));
+    HIP_TRY(hipStreamSynchronize(sc->home.stream));
     *samples_done = sc->ckpt_done;
     return RT_OK;
 }
@@ -514,29 +701,33 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
     int rc = check_settings(s, &cw, &ch);
     if (!rc) rc = check_accel(sc, s);
     if (rc) return rc;
-    HIP_TRY(hipSetDevice(sc->device));
+    if (s->device_count > 1)
+        return fail(RT_ERR_INVALID, "rt_trace_device traces on the scene's device (device_count %d): split the "
+                    "samples over processes, or use rt_render", s->device_count);
+    DeviceState& ds = sc->home;
+    HIP_TRY(hipSetDevice(ds.device));
     // NULL is the default (null) stream, as for rt_finalize_device: the caller's zeroing of d_sum and
     // its reduce / epilogue on that stream are ordered with this trace (the scene's own non-blocking
     // stream would not be: a zeroing enqueued on the default stream could run after the trace's
-    // accumulate pass)
+    // reduce pass)
     hipStream_t st = (hipStream_t)hip_stream;
-    HIP_TRY(sc->total.ensure(kTotalSlots));
+    HIP_TRY(ds.total.ensure(kTotalSlots));
     ImageParams im = image_params(s, cw, ch);
-    Counters c{d_sum, nullptr, nullptr, sc->total.p};
-    if (s->max_depth > 0 && (rc = ensure_partials(sc, s, cw, ch, im.s_end - im.s_begin, c))) return rc;
-    HIP_TRY(order_scratch(sc, st));
-    HIP_TRY(hipMemsetAsync(sc->total.p, 0, kTotalSlots * sizeof(unsigned long long), st));
-    HIP_TRY(hipEventRecord(sc->ev[0], st));
-    HIP_TRY(trace(sc, s, im, c, st));
-    HIP_TRY(hipEventRecord(sc->ev[1], st));
+    Counters c{d_sum, nullptr, nullptr, ds.total.p};
+    if (s->max_depth > 0 && (rc = ensure_partials(sc, ds, cw, ch, im.s_end - im.s_begin, c))) return rc;
+    HIP_TRY(order_scratch(ds, st));
+    HIP_TRY(hipMemsetAsync(ds.total.p, 0, kTotalSlots * sizeof(unsigned long long), st));
+    HIP_TRY(hipEventRecord(ds.ev[0], st));
+    HIP_TRY(trace(sc, ds, s, im, c, st));
+    HIP_TRY(hipEventRecord(ds.ev[1], st));
     unsigned long long totals[kTotalSlots] = {};
-    if (sync || stats) HIP_TRY(hipMemcpyAsync(totals, sc->total.p, sizeof totals, hipMemcpyDeviceToHost, st));
-    HIP_TRY(release_scratch(sc, st));
+    if (sync || stats) HIP_TRY(hipMemcpyAsync(totals, ds.total.p, sizeof totals, hipMemcpyDeviceToHost, st));
+    HIP_TRY(release_scratch(ds, st));
     if (sync || stats) {
         HIP_TRY(hipStreamSynchronize(st));
         if (stats) {
             float ms = 0;
-            HIP_TRY(hipEventElapsedTime(&ms, sc->ev[0], sc->ev[1]));
+            HIP_TRY(hipEventElapsedTime(&ms, ds.ev[0], ds.ev[1]));
             stats->kernel_ms = ms;
             stats->finalize_ms = 0;
             fill_stats(stats, sc, s, totals, (size_t)cw * ch, im);
@@ -552,7 +743,7 @@ int rt_finalize_device(rt_scene* sc, const rt_settings* s, const double* d_sum, 
     int cw, ch;
     int rc = check_settings(s, &cw, &ch);
     if (rc) return rc;
-    HIP_TRY(hipSetDevice(sc->device));
+    HIP_TRY(hipSetDevice(sc->home.device));
     HIP_TRY(epilogue(sc, s, cw, ch, d_sum, d_mean, d_post, d_rgba8, (hipStream_t)hip_stream));
     return RT_OK;
 }

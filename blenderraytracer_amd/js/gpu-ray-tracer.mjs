@@ -45,6 +45,8 @@ export function settingsOf(rt, opts = {}) {
         precision: PRECISION[opts.precision || 'f64'],
         batchSamples: opts.batchSamples || 0,
         accel: ACCEL[opts.accel || 'auto'],
+        // multi-GPU: every sample batch split over these HIP devices (rt_settings.devices)
+        devices: opts.devices ? Array.from(opts.devices) : [],
         // continue a cancelled render from its checkpoint ({sums, samplesDone}, rt_render_resume)
         ...(opts.resume ? { resumeSums: opts.resume.sums, resumeSamplesDone: opts.resume.samplesDone } : {}),
         cropX0: opts.crop ? opts.crop[0] : 0, cropY0: opts.crop ? opts.crop[1] : 0,
@@ -59,17 +61,43 @@ export function settingsOf(rt, opts = {}) {
 
 const isCancelled = () => typeof window !== 'undefined' && window && window.renderCancelled;
 
+const bytesOf = (a) => Buffer.from(a.buffer, a.byteOffset, a.byteLength);
+function samePacked(a, b) {
+    if (!a || !b) return false;
+    for (const k of ['objects', 'materials', 'triangles', 'camera', 'solidColor', 'perm'])
+        if (!bytesOf(a[k]).equals(bytesOf(b[k]))) return false;
+    return a.cameraType === b.cameraType && a.background === b.background && Object.is(a.skyIntensity, b.skyIntensity);
+}
+
+// The scene resident on the GPU for this RayTracer: packed from world / camera at every render (cheap)
+// and compared byte for byte with the cached one, so the upload and the BVH build happen only when
+// the scene or the camera changed (presets, loadFromJSON, updateCamera, updateBackground...).
+function residentScene(rt, nat, device) {
+    const packed = packScene(rt.world, rt.camera);
+    const c = rt.__gpuScene;
+    if (c && c.device === device && samePacked(c.packed, packed)) return c.scene;
+    if (c) nat.destroyScene(c.scene);
+    rt.__gpuScene = null;
+    const scene = nat.createScene(packed, device);
+    Object.defineProperty(rt, '__gpuScene', { value: { scene, packed, device }, writable: true, configurable: true, enumerable: false });
+    return scene;
+}
+
+// Drop the GPU copy of the scene (it is also freed when the RayTracer is garbage collected).
+export function releaseGpuScene(rt) {
+    if (rt.__gpuScene) { loadNative().destroyScene(rt.__gpuScene.scene); rt.__gpuScene = null; }
+}
+
 // The GPU body of render(): trace, epilogue and readback; returns the native result (or null when
 // cancelled, like the reference which then stops silently, ray-tracer.js:256,264).
 export async function gpuRender(rt, onProgress, opts = {}) {
     const nat = loadNative();
-    const scene = nat.createScene(packScene(rt.world, rt.camera), opts.device || 0);
+    const scene = residentScene(rt, nat, opts.device || 0);
     try {
-        const res = await nat.render(scene, settingsOf(rt, opts), (f) => {
+        return await nat.render(scene, settingsOf(rt, opts), (f) => {
             if (onProgress) onProgress(f);
             if (isCancelled()) nat.cancel(scene);
         });
-        return res;
     } catch (e) {
         if (e && e.status === -4) {                               // RT_ERR_CANCELLED
             // keep the progressive state: render({resume: rt.checkpointState}) continues from it
@@ -77,8 +105,6 @@ export async function gpuRender(rt, onProgress, opts = {}) {
             return null;
         }
         throw e;
-    } finally {
-        nat.destroyScene(scene);
     }
 }
 
@@ -90,6 +116,7 @@ function blit(rt, res) {
 }
 
 // Option 1: swap the render() of a reference RayTracer instance for the GPU path.
+// opts: {seed, precision: 'f64'|'f32', accel, batchSamples, device, devices: [HIP ordinals]}
 export function installGpuRender(rayTracer, opts = {}) {
     rayTracer.render = async function render(onProgress) {
         const res = await gpuRender(this, onProgress, opts);

@@ -17,7 +17,7 @@ from .scene import PackedScene, default_scene, load_from_json, setup_camera, key
 
 def settings_struct(width, height, samples, max_bounces, anti_aliasing, tone_mapping, exposure, gamma, seed,
                     crop=None, precision=capi.RT_PREC_F64, sample_range=None, batch_samples=0, denoising=False,
-                    denoise_strength=0.5, accel=capi.RT_ACCEL_AUTO):
+                    denoise_strength=0.5, accel=capi.RT_ACCEL_AUTO, devices=None):
     """rt_settings from RayTracer fields, resolving sampleCount (ray-tracer.js:201) and the string
     switches of getAntiAliasSample (:125-149) and toneMap (:151-161)."""
     s = capi.Settings()
@@ -36,6 +36,12 @@ def settings_struct(width, height, samples, max_bounces, anti_aliasing, tone_map
     s.precision = int(precision)
     s.batch_samples = int(batch_samples)
     s.accel = int(accel)
+    if devices:                 # multi-GPU sample split (rt_settings.devices)
+        if len(devices) > capi.RT_MAX_DEVICES:
+            raise ValueError(f"at most {capi.RT_MAX_DEVICES} devices")
+        s.device_count = len(devices)
+        for k, d in enumerate(devices):
+            s.devices[k] = int(d)
     if truthy(denoising):
         # post-processor.js:55: Math.exp(-(kx*kx + ky*ky) / (2 * strength * strength)) for kx^2+ky^2 = 1, 2
         st = float(denoise_strength)
@@ -107,11 +113,12 @@ class GpuRayTracer:
             self._packed = PackedScene(self.world, self.camera)
         return self._packed
 
-    def settings(self, crop=None, sample_range=None, batch_samples=0):
+    def settings(self, crop=None, sample_range=None, batch_samples=0, devices=None):
         return settings_struct(self.width, self.height, self.samples, self.max_bounces, self.anti_aliasing,
                                self.tone_mapping, self.exposure, self.gamma, self.seed, crop=crop,
                                precision=self.precision, sample_range=sample_range, batch_samples=batch_samples,
-                               denoising=self.denoising, denoise_strength=self.denoise_strength, accel=self.accel)
+                               denoising=self.denoising, denoise_strength=self.denoise_strength, accel=self.accel,
+                               devices=devices)
 
     def scene_handle(self):
         lib = capi.load_library()
@@ -123,13 +130,14 @@ class GpuRayTracer:
             self._dirty = False
         return self._scene
 
-    def render(self, on_progress=None, crop=None, want=("rgba8",), batch_samples=0, resume=None):
+    def render(self, on_progress=None, crop=None, want=("rgba8",), batch_samples=0, resume=None, devices=None):
         """RayTracer.render: fills image_data (RGBA8) and float_data (post-gamma RGBA float).
         Returns a dict of the requested host arrays (mean, post, rgba8, segments, draws).
-        resume: a checkpoint() result to continue from (rt_render_resume)."""
+        resume: a checkpoint() result to continue from (rt_render_resume).
+        devices: HIP ordinals to split every sample batch over (multi-GPU; may repeat a device)."""
         lib = capi.load_library()
         scene = self.scene_handle()
-        st = self.settings(crop=crop, batch_samples=batch_samples)
+        st = self.settings(crop=crop, batch_samples=batch_samples, devices=devices)
         cw = st.crop_w or self.width
         ch = st.crop_h or self.height
         n = cw * ch

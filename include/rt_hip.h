@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2      /* 2: rt_settings.device_count / devices (multi-GPU sample split) */
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -62,6 +62,8 @@ typedef enum rt_background_type {
     RT_BG_NAN = 4              /* JSON "solid"/"hdri": the loader binds a factory, radiance is NaN
                                   (scene-loader.js:41-45) */
 } rt_background_type;
+
+#define RT_MAX_DEVICES 8
 
 typedef enum rt_camera_type { RT_CAM_PERSPECTIVE = 0, RT_CAM_ORTHOGRAPHIC = 1 } rt_camera_type;
 /* getAntiAliasSample (ray-tracer.js:125-149): any string other than 'stochastic' and
@@ -145,7 +147,15 @@ typedef struct rt_settings {
     double denoise_weights[2]; /* Math.exp(-1/(2s*s)), Math.exp(-2/(2s*s)), s = denoiseStrength, evaluated by
                                   the host with its own exp (post-processor.js:55) */
     int32_t accel;             /* rt_accel: how World.hit is evaluated (results are identical) */
-    int32_t _pad;
+    int32_t device_count;      /* 0 or 1: the scene's own device.  N in 2..RT_MAX_DEVICES: every sample
+                                  batch is split into N contiguous sample ranges, range k traced on HIP
+                                  device devices[k], the per-pixel float64 sums added on the
+                                  scene's device in range order (peer copies over xGMI), then the epilogue.
+                                  A device may be listed more than once (its ranges run on separate
+                                  streams).  The scene is uploaded to each listed device on first use and
+                                  kept.  Equal to one device up to the order of the binary64 additions. */
+    int32_t devices[8];        /* HIP ordinals of the devices (device_count of them) */
+    int32_t _pad2;
 } rt_settings;
 
 /* Host outputs of rt_render, each optional (NULL = not wanted). n = crop_w*crop_h pixels,
@@ -189,7 +199,11 @@ void rt_scene_destroy(rt_scene* scene);
 /* Full render into host buffers: trace, finalize (tone map, gamma, RGBA8) and copy back.
  * Replaces RayTracer.render (ray-tracer.js:166-281) minus the DOM. Synchronous.
  * progress(fraction, user) is called between sample batches from the calling thread; a non-zero
- * return value cancels (like window.renderCancelled, ray-tracer.js:190,196). */
+ * return value cancels (like window.renderCancelled, ray-tracer.js:190,196).
+ * Threading: one call in flight per scene (rt_render, rt_render_resume, rt_trace_device,
+ * rt_finalize_device, rt_render_checkpoint), as for the reference's render(); calls on different
+ * scenes may run concurrently from different threads.  Asynchronous device calls on different streams
+ * are ordered by the scene itself (its scratch buffers are event-guarded). */
 typedef int (*rt_progress_fn)(double fraction, void* user);
 int rt_render(rt_scene* scene, const rt_settings* settings, const rt_output* out,
               rt_progress_fn progress, void* user, rt_stats* stats);

@@ -72,6 +72,30 @@ if (cmd === 'pack') {
         const a = full.imageData.data, b = part.imageData.data;
         summary._resume = { samplesDone: done, equal: a.length === b.length && a.every((v, i) => v === b[i]) };
     }
+    // multi-GPU through the drop-in: settings.devices = [0, 0] (two sample ranges on this GPU), and
+    // the scene upload cached across render() calls
+    {
+        const { rt: one } = tracerFor('kitchen_sink');
+        const a = await one.renderBuffers({ wantMean: true, wantCounts: true });
+        const { rt: two } = tracerFor('kitchen_sink', { devices: [0, 0] });
+        const b = await two.renderBuffers({ wantMean: true, wantCounts: true });
+        const sceneBefore = two.__gpuScene && two.__gpuScene.scene;
+        await two.render();
+        const sceneAfter = two.__gpuScene && two.__gpuScene.scene;
+        two.updateBackground('procedural_sky', 1.0);                     // a change re-uploads
+        await two.render();
+        let maxRel = 0;
+        for (let i = 0; i < a.mean.length; i++) {
+            if (Number.isNaN(a.mean[i]) && Number.isNaN(b.mean[i])) continue;
+            maxRel = Math.max(maxRel, Math.abs(a.mean[i] - b.mean[i]) / Math.max(1, Math.abs(a.mean[i])));
+        }
+        summary._devices = {
+            maxRel, segsEqual: a.segments.every((v, i) => v === b.segments[i]),
+            drawsEqual: a.draws.every((v, i) => v === b.draws[i]),
+            sceneCached: sceneBefore !== undefined && sceneBefore === sceneAfter,
+            reuploaded: two.__gpuScene.scene !== sceneAfter,
+        };
+    }
     fs.writeFileSync(path.join(outdir, 'summary.json'), JSON.stringify(summary));
 } else if (cmd === 'refpack') {
     // The drop-in: the reference's own RayTracer (temp copy prepared by the caller), its render()

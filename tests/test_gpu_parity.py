@@ -361,3 +361,80 @@ def test_sharded_step_matches_render(gpu):
         job.step(stats=False)
         torch.cuda.synchronize()
         assert np.array_equal(job.rgba8.cpu().numpy().reshape(ref.shape), ref)
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]], ids=["2_shards", "3_shards"])
+def test_multi_device_split_matches_one_device(gpu, devices):
+    """rt_settings.devices (SURVEY §8e through the C ABI): every sample batch split into contiguous
+    sample ranges, one per listed device (here all device 0: the replicas run on their own streams),
+    sums merged on the scene's device in range order.  Equal to one device up to summation order, with
+    identical per-pixel segment and draw counts; also with sample batches (progress granularity)."""
+    rt = _rtow(160, 90, 24)
+    want = ("mean", "segments", "draws")
+    one = rt.render(want=want)
+    many = rt.render(want=want, devices=devices)
+    for k in ("segments", "draws"):
+        assert np.array_equal(one[k], many[k]), k
+    assert np.allclose(one["mean"], many["mean"], rtol=SUM_RTOL, atol=0)
+    batched = rt.render(want=want, devices=devices, batch_samples=7)
+    assert np.array_equal(one["segments"], batched["segments"])
+    assert np.allclose(one["mean"], batched["mean"], rtol=SUM_RTOL, atol=0)
+    again = rt.render(want=want, devices=devices, batch_samples=7)      # replicas cached, re-zeroed
+    assert np.array_equal(batched["mean"], again["mean"])
+    rt.close()
+
+
+def test_multi_device_checkpoint_resume(gpu):
+    """Cancel a 2-device render between batches, checkpoint the merged sums, resume in a new scene
+    with the same devices and batches: bit-identical to the uninterrupted render."""
+    rt = _rtow(96, 54, 10)
+    full = rt.render(want=("mean",), batch_samples=3, devices=[0, 0])
+    calls = []
+    with pytest.raises(RuntimeError, match="CANCELLED"):
+        rt.render(batch_samples=3, devices=[0, 0], on_progress=lambda f: calls.append(f) or len(calls) >= 2)
+    sums, done = rt.checkpoint()
+    assert done == 6
+    rt.close()
+    rt2 = _rtow(96, 54, 10)
+    res = rt2.render(want=("mean",), resume=(sums, done), batch_samples=3, devices=[0, 0])
+    assert np.array_equal(res["mean"], full["mean"])
+    rt2.close()
+
+
+def test_config4_rtow_4k_1024spp_sharded(gpu):
+    """Config 4 at its full size: RTOW 3840x2160 x 1024 spp (8.5e9 samples).  (1) Through
+    rt_trace_device, 8 sample-range shards (the per-GPU work of the 8-GPU split, run one after another
+    on this GPU) add up to the single-launch sums (ray-tracer.js:202-206 is a per-pixel sum over
+    samples, so only the summation order may differ).  (2) Through rt_render with devices=[0]*8 (the
+    C ABI's own split).  (3) Three 16x16 windows of the sharded frame match the oracle at full 1024 spp
+    (segment counts identical, means within 1e-12)."""
+    import torch
+    W, H, S = 3840, 2160, 1024
+    rt = _rtow(W, H, S, seed=4)
+    lib = capi.load_library()
+    scene = rt.scene_handle()
+    n = W * H
+    full = torch.zeros(n * 3, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    capi.check(lib.rt_trace_device(scene, C.byref(rt.settings()), C.c_void_p(full.data_ptr()), None, 1, None))
+    shards = torch.zeros(n * 3, dtype=torch.float64, device="cuda")
+    part = torch.zeros(n * 3, dtype=torch.float64, device="cuda")
+    for k in range(8):
+        part.zero_()
+        torch.cuda.synchronize()
+        rng = (k * S // 8, (k + 1) * S // 8)
+        capi.check(lib.rt_trace_device(scene, C.byref(rt.settings(sample_range=rng)), C.c_void_p(part.data_ptr()), None, 1, None))
+        shards += part
+    torch.cuda.synchronize()
+    a, b = full.cpu().numpy().reshape(H, W, 3), shards.cpu().numpy().reshape(H, W, 3)
+    assert np.all(np.isfinite(a))
+    assert np.allclose(a, b, rtol=SUM_RTOL, atol=0)
+    del full, shards, part
+    r = rt.render(want=("mean",), devices=[0] * 8)
+    assert np.allclose(r["mean"], a / S, rtol=SUM_RTOL, atol=0)
+    for (x0, y0) in ((0, 0), (1900, 1060), (3824, 2144)):
+        o = binding.render(rt.packed(), rt.settings(crop=(x0, y0, 16, 16)))
+        g = rt.render(want=("mean", "segments"), crop=(x0, y0, 16, 16))
+        assert np.array_equal(o["segments"], g["segments"])
+        assert rel_err(b[y0:y0 + 16, x0:x0 + 16] / S, o["mean"]) <= 1e-12
+    rt.close()

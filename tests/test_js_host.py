@@ -127,7 +127,7 @@ def test_js_packing_of_real_reference_objects():
 def test_addon_loads_without_gpu_and_fails_loudly():
     if not os.path.exists(ADDON):
         pytest.skip("rt_napi.node not built")
-    code = ("const m=require(%r); if (m.abiVersion()!==1) process.exit(3);"
+    code = ("const m=require(%r); if (m.abiVersion()!==2) process.exit(3);"
             "if (m.deviceCount()===0) { try { m.createScene({camera:new Float64Array(22),perm:new Int32Array(512)},0);"
             " process.exit(4);} catch(e) { if(!/no HIP device/.test(e.message)) process.exit(5);} }") % ADDON
     r = subprocess.run([NODE, "-e", code], capture_output=True)
@@ -161,4 +161,7 @@ def test_js_gpu_render_matches_reference(gpu):
         # the deterministic cancel / checkpoint / resume check is test_gpu_parity.py's
         # test_checkpoint_resume_is_bit_exact
         assert summary["_resume"]["equal"] is True
+        dv = summary["_devices"]                    # settings.devices = [0, 0] through N-API
+        assert dv["segsEqual"] and dv["drawsEqual"] and dv["maxRel"] <= 1e-13, dv
+        assert dv["sceneCached"] and dv["reuploaded"], dv
         assert summary["_resume"]["samplesDone"] in (4, 6, 8)
