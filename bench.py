@@ -195,6 +195,35 @@ def pmc_passes(args, outdir):
     return res
 
 
+def node_end_to_end(cfg, args):
+    """The Node drop-in end to end (scripts/node_e2e.mjs): GpuRayTracer.render() through rt_napi.node,
+    scene resident from the first call, timed on the second."""
+    import shutil
+    import subprocess
+    import tempfile
+    node = shutil.which("node")
+    if node is None or not os.path.exists(os.path.join(ROOT, "blenderraytracer_amd", "lib", "rt_napi.node")):
+        return {"error": "node or rt_napi.node not available"}
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+        json.dump(load_scene_json(cfg["scene"]), f)
+        path = f.name
+    try:
+        a = dict(scene=path, width=cfg["w"], height=cfg["h"], spp=cfg["spp"], depth=cfg["depth"], seed=args.seed,
+                 precision=args.precision)
+        r = subprocess.run([node, os.path.join(ROOT, "scripts", "node_e2e.mjs"), json.dumps(a)], capture_output=True,
+                           text=True, timeout=600)
+        if r.returncode != 0:
+            return {"error": r.stderr[-300:]}
+        out = json.loads(r.stdout)
+    finally:
+        os.unlink(path)
+    return {"value": round(out["value"], 3), "unit": "Msamples/s", "wall_ms": round(out["wall_ms"], 3),
+            "first_call_ms": round(out["first_call_ms"], 3), "kernel_ms": out["kernel_ms"],
+            "what": "GpuRayTracer.render() from Node (the installGpuRender path): scene resident from the first call "
+                    "(first_call_ms includes its upload and BVH build), pack + compare, trace, epilogue, RGBA8 + "
+                    "Float32 readback"}
+
+
 def git_head():
     try:
         import subprocess
@@ -249,7 +278,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    e2e = None
+    e2e = e2e_node = None
     if rank == 0 and world == 1 and not args.no_end_to_end:
         # RayTracer.render as the drop-in boundary runs it (rt_render): sums zeroed on device, the
         # trace, the epilogue, Float32 post-gamma + RGBA8 frames copied back over PCIe
@@ -260,6 +289,7 @@ def main():
         e2e = {"value": round(cfg["w"] * cfg["h"] * rt.settings().samples / wall / 1e6, 3), "unit": "Msamples/s",
                "wall_ms": round(wall * 1e3, 3), "kernel_ms": round(rt.last_stats.kernel_ms, 3),
                "what": "one rt_render call from Python: trace + tone map/gamma/RGBA8 + Float32 and RGBA8 readback"}
+        e2e_node = node_end_to_end(cfg, args)
 
     if rank == 0:
         total_samples = cfg["w"] * cfg["h"] * rt.settings().samples * args.steps
@@ -345,6 +375,7 @@ def main():
             "kernel_msamples_per_s": round(rank_samples / (k_ms * 1e-3) / 1e6, 3),
             "cpu_baseline": cpu,
             "end_to_end": e2e,
+            "end_to_end_node": e2e_node,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -70,8 +70,12 @@ RT_HD void start_sample(const SceneView<R>& sc, const ImageParams& im, int i, in
 }
 
 // x^5 for Schlick's approximation (materials.js:79-83, Math.pow(1 - cosine, 5)), correctly rounded.
-// Neither V8's Math.pow (fdlibm) nor glibc's pow is always correctly rounded (both <= ~0.5 ulp), and
-// the device pow (ocml, <= 1 ulp) costs ~100 binary64 instructions.  Here x^2, x^4, x^5 are carried
+// The reference's own Math.pow (V8 in Node 12) is not: it differs from RN(x^5) by 1 ulp in ~9 % of
+// arguments (glibc in 0.08 %; tests/test_js_host.py::test_pow5_vs_v8_math_pow), so this value is not
+// bit-pinned to the reference.  The path only uses it in `reflectance > Math.random()`, whose draws are
+// multiples of 2^-24: a 1-ulp difference flips that decision only if the reflectance is within 1 ulp
+// of such a multiple (none of 100k test arguments; every golden fixture's decisions identical).  The
+// device pow (ocml, <= 1 ulp) costs ~100 binary64 instructions.  Here x^2, x^4, x^5 are carried
 // as unevaluated sums hi + lo (error-free products by FMA): the pair approximates x^5 to ~2^-100
 // relative, so the single final rounding gives RN(x^5) unless x^5 lies within 2^-100 of a rounding
 // midpoint.  10 binary64 ops; exact for x = 0 and x = 1.  Checked against exact rationals

@@ -165,3 +165,42 @@ def test_js_gpu_render_matches_reference(gpu):
         assert dv["segsEqual"] and dv["drawsEqual"] and dv["maxRel"] <= 1e-13, dv
         assert dv["sceneCached"] and dv["reuploaded"], dv
         assert summary["_resume"]["samplesDone"] in (4, 6, 8)
+
+
+def test_pow5_vs_v8_math_pow(tmp_path):
+    """pt_path.h's pow5_rn (the kernel's Schlick x^5, correctly rounded) against the reference's own
+    Math.pow(x, 5) under this Node's V8 (materials.js:82) on 100k arguments over the dielectric's range.
+    V8's pow (Node 12) is not correctly rounded: it differs by 1 ulp in ~9 % of these arguments (glibc:
+    0.08 %), so the kernel's x^5 is NOT bit-pinned to the reference (parity unpinned for this value).
+    What the path consumes is only the decision reflectance > Math.random() (draws are multiples of
+    2^-24): the test computes Schlick's reflectance (materials.js:79-83, ior 1.5 and 1/1.5) with both x^5
+    and asserts that no mismatch straddles a multiple of 2^-24, i.e. no decision flips on this sample."""
+    import ctypes as C
+    import hostcheck_binding as hb
+    rng = np.random.default_rng(5)
+    c = np.concatenate([rng.uniform(-1.0, 1.0, 60_000), 1.0 - rng.uniform(0, 1e-3, 20_000), rng.uniform(0, 1, 20_000) ** 8])
+    x = np.concatenate([1.0 - c, [0.0, 1.0, 2.0, 2.0 ** -53, 0.5, 1.5, 1e-16]])
+    xin, xout = tmp_path / "x.bin", tmp_path / "v8.bin"
+    x.tofile(xin)
+    code = ("const fs=require('fs');const b=fs.readFileSync(%r);const x=new Float64Array(b.buffer,b.byteOffset,b.length/8);"
+            "const y=new Float64Array(x.length);for(let i=0;i<x.length;i++)y[i]=Math.pow(x[i],5);"
+            "fs.writeFileSync(%r,Buffer.from(y.buffer));") % (str(xin), str(xout))
+    subprocess.run([NODE, "-e", code], check=True, timeout=120)
+    v8 = np.fromfile(xout, dtype=np.float64)
+    L = hb.lib()
+    L.ptc_pow5.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_longlong]
+    ours = np.empty_like(x)
+    L.ptc_pow5(x.ctypes.data_as(C.POINTER(C.c_double)), ours.ctypes.data_as(C.POINTER(C.c_double)), len(x))
+    diff = ours != v8
+    print(f"pow5_rn vs V8 Math.pow(x, 5): {int(diff.sum())} of {len(x)} differ ({diff.mean():.2e})")
+    assert diff.mean() <= 0.15
+    assert np.all(np.abs(ours[diff] - v8[diff]) <= np.spacing(np.abs(v8[diff])))
+    flips = 0
+    for ior in (1.5, 1 / 1.5):
+        r0 = (1 - ior) / (1 + ior)
+        r0 = r0 * r0
+        ra, rb = r0 + (1 - r0) * ours[diff], r0 + (1 - r0) * v8[diff]
+        lo, hi = np.minimum(ra, rb), np.maximum(ra, rb)
+        flips += int(np.sum(np.ceil(lo * 2.0 ** 24) < hi * 2.0 ** 24))    # a draw u*2^-24 in [lo, hi)
+    print(f"Schlick decisions flipped by the x^5 mismatches: {flips}")
+    assert flips == 0
