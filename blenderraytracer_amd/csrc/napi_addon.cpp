@@ -187,10 +187,14 @@ struct RenderJob {
     rt_settings st{};
     size_t n = 0;
     bool want_mean = false, want_counts = false;
-    std::vector<double> mean;
-    std::vector<float> post;
-    std::vector<uint8_t> rgba;
-    std::vector<uint32_t> segs, draws;
+    // outputs live in JS ArrayBuffers created on the main thread before the work is queued (kept alive
+    // by references, not visible to JS until the promise resolves): rt_render copies the frames from
+    // HBM straight into them, with no staging vectors and no copy into the result.  settings.outRgba8
+    // (the caller's imageData.data) receives the RGBA8 frame in place.
+    enum { OUT_POST, OUT_RGBA, OUT_MEAN, OUT_SEGS, OUT_DRAWS, OUT_N };
+    napi_ref out_ref[OUT_N] = {};
+    void* out_ptr[OUT_N] = {};
+    bool rgba_is_caller = false;
     rt_stats stats{};
     int status = 0;
     std::string error;
@@ -219,26 +223,33 @@ int progress_hook(double fraction, void* user) {
 void execute(napi_env, void* data) {
     RenderJob* job = static_cast<RenderJob*>(data);
     rt_output out{};
-    job->post.resize(job->n * 4);
-    job->rgba.resize(job->n * 4);
-    out.post = job->post.data();
-    out.rgba8 = job->rgba.data();
-    if (job->want_mean) {
-        job->mean.resize(job->n * 3);
-        out.mean = job->mean.data();
-    }
-    if (job->want_counts) {
-        job->segs.resize(job->n);
-        job->draws.resize(job->n);
-        out.segments = job->segs.data();
-        out.draws = job->draws.data();
-    }
+    out.post = static_cast<float*>(job->out_ptr[RenderJob::OUT_POST]);
+    out.rgba8 = static_cast<uint8_t*>(job->out_ptr[RenderJob::OUT_RGBA]);
+    out.mean = static_cast<double*>(job->out_ptr[RenderJob::OUT_MEAN]);
+    out.segments = static_cast<uint32_t*>(job->out_ptr[RenderJob::OUT_SEGS]);
+    out.draws = static_cast<uint32_t*>(job->out_ptr[RenderJob::OUT_DRAWS]);
     if (job->resume_done >= 0)
         job->status = rt_render_resume(job->scene, &job->st, job->resume.data(), job->resume_done, &out, progress_hook,
                                        job, &job->stats);
     else
         job->status = rt_render(job->scene, &job->st, &out, progress_hook, job, &job->stats);
     if (job->status != RT_OK) job->error = rt_last_error();
+}
+
+// A new ArrayBuffer of `bytes` on the main thread, referenced by the job until it completes.
+bool make_out(napi_env env, RenderJob* job, int slot, size_t bytes) {
+    napi_value ab;
+    if (napi_create_arraybuffer(env, bytes, &job->out_ptr[slot], &ab) != napi_ok) return false;
+    return napi_create_reference(env, ab, 1, &job->out_ref[slot]) == napi_ok;
+}
+
+// The typed array over output slot `slot` (the ArrayBuffer, or the caller's own typed array).
+napi_value out_array(napi_env env, RenderJob* job, int slot, napi_typedarray_type t, size_t len) {
+    napi_value v, arr;
+    napi_get_reference_value(env, job->out_ref[slot], &v);
+    if (slot == RenderJob::OUT_RGBA && job->rgba_is_caller) return v;
+    napi_create_typedarray(env, t, len, v, 0, &arr);
+    return arr;
 }
 
 template <class T>
@@ -264,12 +275,12 @@ void complete(napi_env env, napi_status, void* data) {
     } else {
         napi_value res, stats, v;
         napi_create_object(env, &res);
-        napi_set_named_property(env, res, "post", to_typed(env, job->post, napi_float32_array));
-        napi_set_named_property(env, res, "rgba8", to_typed(env, job->rgba, napi_uint8_clamped_array));
-        if (job->want_mean) napi_set_named_property(env, res, "mean", to_typed(env, job->mean, napi_float64_array));
+        napi_set_named_property(env, res, "post", out_array(env, job, RenderJob::OUT_POST, napi_float32_array, job->n * 4));
+        napi_set_named_property(env, res, "rgba8", out_array(env, job, RenderJob::OUT_RGBA, napi_uint8_clamped_array, job->n * 4));
+        if (job->want_mean) napi_set_named_property(env, res, "mean", out_array(env, job, RenderJob::OUT_MEAN, napi_float64_array, job->n * 3));
         if (job->want_counts) {
-            napi_set_named_property(env, res, "segments", to_typed(env, job->segs, napi_uint32_array));
-            napi_set_named_property(env, res, "draws", to_typed(env, job->draws, napi_uint32_array));
+            napi_set_named_property(env, res, "segments", out_array(env, job, RenderJob::OUT_SEGS, napi_uint32_array, job->n));
+            napi_set_named_property(env, res, "draws", out_array(env, job, RenderJob::OUT_DRAWS, napi_uint32_array, job->n));
         }
         napi_create_object(env, &stats);
         const struct { const char* k; double v; } fields[] = {
@@ -285,6 +296,8 @@ void complete(napi_env env, napi_status, void* data) {
         napi_resolve_deferred(env, job->deferred, res);
     }
     job->box->busy = false;
+    for (napi_ref r : job->out_ref)
+        if (r) napi_delete_reference(env, r);
     napi_delete_reference(env, job->scene_ref);
     napi_delete_async_work(env, job->work);
     delete job;
@@ -349,6 +362,28 @@ napi_value render(napi_env env, napi_callback_info info) {
         }
         job->resume.assign(static_cast<double*>(rs), static_cast<double*>(rs) + job->n * 3);
         job->resume_done = (int32_t)get_num(env, s, "resumeSamplesDone", 0);
+    }
+    // output buffers (see RenderJob): post always, RGBA8 into settings.outRgba8 when it is the frame's size
+    bool ok = make_out(env, job, RenderJob::OUT_POST, job->n * 4 * sizeof(float));
+    void* rgba_p = nullptr;
+    size_t rgba_bytes = 0;
+    napi_value rgba_v;
+    if (ok && get_bytes(env, s, "outRgba8", &rgba_p, &rgba_bytes) && rgba_bytes == job->n * 4 &&
+        get_prop(env, s, "outRgba8", &rgba_v)) {
+        job->out_ptr[RenderJob::OUT_RGBA] = rgba_p;
+        job->rgba_is_caller = true;
+        ok = napi_create_reference(env, rgba_v, 1, &job->out_ref[RenderJob::OUT_RGBA]) == napi_ok;
+    } else if (ok) {
+        ok = make_out(env, job, RenderJob::OUT_RGBA, job->n * 4);
+    }
+    if (ok && job->want_mean) ok = make_out(env, job, RenderJob::OUT_MEAN, job->n * 3 * sizeof(double));
+    if (ok && job->want_counts) ok = make_out(env, job, RenderJob::OUT_SEGS, job->n * sizeof(uint32_t)) &&
+                                     make_out(env, job, RenderJob::OUT_DRAWS, job->n * sizeof(uint32_t));
+    if (!ok) {
+        for (napi_ref r : job->out_ref)
+            if (r) napi_delete_reference(env, r);
+        delete job;
+        return throw_err(env, "render: cannot allocate the output buffers");
     }
     box->last_pixels = job->n;
     napi_value promise, name;

@@ -94,7 +94,11 @@ export async function gpuRender(rt, onProgress, opts = {}) {
     const nat = loadNative();
     const scene = residentScene(rt, nat, opts.device || 0);
     try {
-        return await nat.render(scene, settingsOf(rt, opts), (f) => {
+        const st = settingsOf(rt, opts);
+        // render() proper: the RGBA8 frame is written straight into this.imageData.data (full frame only)
+        if (opts.intoImageData && !opts.crop && rt.imageData && rt.imageData.data.length === rt.width * rt.height * 4)
+            st.outRgba8 = rt.imageData.data;
+        return await nat.render(scene, st, (f) => {
             if (onProgress) onProgress(f);
             if (isCancelled()) nat.cancel(scene);
         });
@@ -110,7 +114,7 @@ export async function gpuRender(rt, onProgress, opts = {}) {
 
 function blit(rt, res) {
     // ray-tracer.js:215-276: RGBA8 top-down row-major, alpha 255, denoised when rt.denoising (all on the GPU)
-    rt.imageData.data.set(res.rgba8);
+    if (res.rgba8 !== rt.imageData.data) rt.imageData.data.set(res.rgba8);
     rt.floatData = res.post;
     if (rt.ctx && rt.ctx.putImageData) rt.ctx.putImageData(rt.imageData, 0, 0);
 }
@@ -119,7 +123,7 @@ function blit(rt, res) {
 // opts: {seed, precision: 'f64'|'f32', accel, batchSamples, device, devices: [HIP ordinals]}
 export function installGpuRender(rayTracer, opts = {}) {
     rayTracer.render = async function render(onProgress) {
-        const res = await gpuRender(this, onProgress, opts);
+        const res = await gpuRender(this, onProgress, { ...opts, intoImageData: true });
         if (!res) return;
         blit(this, res);
         this.lastStats = res.stats;
@@ -182,7 +186,7 @@ export class GpuRayTracer {
     }
 
     async render(onProgress) {
-        const res = await gpuRender(this, onProgress, this.opts);
+        const res = await gpuRender(this, onProgress, { ...this.opts, intoImageData: true });
         if (!res) return;
         blit(this, res);
         this.lastStats = res.stats;
@@ -192,7 +196,7 @@ export class GpuRayTracer {
     // Continue the last cancelled render (window.renderCancelled) from its checkpoint.
     async resume(onProgress) {
         if (!this.checkpointState) return this.render(onProgress);
-        const res = await gpuRender(this, onProgress, { ...this.opts, resume: this.checkpointState });
+        const res = await gpuRender(this, onProgress, { ...this.opts, resume: this.checkpointState, intoImageData: true });
         if (!res) return;
         this.checkpointState = null;
         blit(this, res);
