@@ -140,6 +140,8 @@ struct SceneView {
     const Bvh2Node* tri_wide;
     int num_sphere_wide, num_tri_wide;
     int stack_entries;             // deepest leaf of the two trees (>= 1): the ordered walk's stack bound
+    const SphereLeaf<R>* big_spheres;   // dominant spheres kept out of the sphere tree (scene_pack.h)
+    int num_big_spheres;
     // camera (camera.js:8-36 vectors, computed on the host in binary64)
     R cam_o[3], cam_llc[3], cam_h[3], cam_v[3], cam_u[3], cam_vv[3], cam_w[3];
     R lens_radius;
@@ -555,14 +557,13 @@ RT_HD void brute_planes_boxes(const SceneView<R>& sc, V3<R> o, V3<R> d, R tmin, 
     }
 }
 
-// The primitives of one BVH leaf (fc = (first << 4) | count) against the current best.
+// Sphere records [first, end) of `recs` (a BVH leaf, or the dominant spheres) against the current best.
 template <class R>
-RT_HD void sphere_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R a, const FilterRay& fr, R tmin,
-                       Closest<R>& b, float& tl, Work& w) {
-    const int first = fc >> 4, end = first + (fc & 15);
+RT_HD void sphere_records(const SphereLeaf<R>* recs, int first, int end, V3<R> o, V3<R> d, R a, const FilterRay& fr,
+                          R tmin, Closest<R>& b, float& tl, Work& w) {
     RT_COUNT(w.spheres += end - first);
     for (int k = first; k < end; ++k) {
-        const SphereLeaf<R> L = sc.bvh_sphere_leaf[k];
+        const SphereLeaf<R> L = recs[k];
         if constexpr (sizeof(R) == 8)
             if (!sphere_filter_pass(L.f, fr)) continue;
         R t;
@@ -572,6 +573,13 @@ RT_HD void sphere_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R a, co
             tl = bvh_tlimit(b.t);
         }
     }
+}
+
+// The primitives of one BVH leaf (fc = (first << 4) | count) against the current best.
+template <class R>
+RT_HD void sphere_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R a, const FilterRay& fr, R tmin,
+                       Closest<R>& b, float& tl, Work& w) {
+    sphere_records(sc.bvh_sphere_leaf, fc >> 4, (fc >> 4) + (fc & 15), o, d, a, fr, tmin, b, tl, w);
 }
 
 template <class R>
@@ -600,12 +608,15 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
     brute_planes_boxes(sc, o, d, tmin, b);
     const BvhRay br = make_bvh_ray(o, d);
     float tl = bvh_tlimit(b.t);
-    if (sc.num_sphere_nodes > 0) {
+    if (sc.num_sphere_nodes > 0 || sc.num_big_spheres > 0) {
         const R a = dot(d, d);
         FilterRay fr{};
         if constexpr (sizeof(R) == 8) fr = make_filter_ray(o, d);
+        // dominant spheres first: their hit bounds the walk (scene_pack.h peel_big_spheres)
+        if (sc.num_big_spheres > 0) sphere_records(sc.big_spheres, 0, sc.num_big_spheres, o, d, a, fr, tmin, b, tl, w);
         auto leaf = [&](int fc) { sphere_leaf(sc, fc, o, d, a, fr, tmin, b, tl, w); };
-        bvh_walk<WIDE>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w, leaf);
+        if (sc.num_sphere_nodes > 0)
+            bvh_walk<WIDE>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w, leaf);
     }
     if (sc.num_tri_nodes > 0) {
         auto leaf = [&](int fc) { tri_leaf(sc, fc, o, d, tmin, b, tl, w); };

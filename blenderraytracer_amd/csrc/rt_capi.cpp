@@ -98,13 +98,14 @@ struct DeviceScene {
     DevBuf<BvhNode> sphere_nodes, tri_nodes;
     DevBuf<SphereLeaf<R>> bvh_sphere_leaf;
     DevBuf<TriLeaf<R>> bvh_tri_leaf;
+    DevBuf<SphereLeaf<R>> big_sphere_leaf;
     DevBuf<Bvh2Node> sphere_wide, tri_wide;
     SceneView<R> view{};
     void release() {
         runs.release(); spheres.release(); sphere_filter.release(); sphere_r.release(); planes.release(); boxes.release(); tris.release();
         sphere_mat.release(); plane_mat.release(); box_mat.release(); tri_mat.release(); perm.release(); mats.release();
         plane_obj.release(); box_obj.release(); sphere_nodes.release(); tri_nodes.release(); bvh_sphere_leaf.release();
-        bvh_tri_leaf.release();
+        bvh_tri_leaf.release(); big_sphere_leaf.release();
         sphere_wide.release(); tri_wide.release();
     }
 };
@@ -119,7 +120,7 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     UP(boxes, rec.boxes); UP(tris, rec.tris); UP(sphere_mat, hs.sphere_mat); UP(plane_mat, hs.plane_mat);
     UP(box_mat, hs.box_mat); UP(tri_mat, hs.tri_mat); UP(perm, rec.perm); UP(mats, rec.mats);
     UP(plane_obj, hs.plane_obj); UP(box_obj, hs.box_obj); UP(sphere_nodes, hs.sphere_bvh); UP(tri_nodes, hs.tri_bvh);
-    UP(bvh_sphere_leaf, rec.bvh_sphere_leaf); UP(bvh_tri_leaf, rec.bvh_tri_leaf); UP(sphere_wide, hs.sphere_wide); UP(tri_wide, hs.tri_wide);
+    UP(bvh_sphere_leaf, rec.bvh_sphere_leaf); UP(bvh_tri_leaf, rec.bvh_tri_leaf); UP(big_sphere_leaf, rec.big_sphere_leaf); UP(sphere_wide, hs.sphere_wide); UP(tri_wide, hs.tri_wide);
 #undef UP
     if (e != hipSuccess) return fail(RT_ERR_DEVICE, "scene upload: %s", hipGetErrorString(e));
     SceneView<R>& v = ds.view;
@@ -129,6 +130,7 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     v.tri_mat = ds.tri_mat.p; v.mats = ds.mats.p; v.perm = ds.perm.p;
     v.plane_obj = ds.plane_obj.p; v.box_obj = ds.box_obj.p; v.sphere_nodes = ds.sphere_nodes.p; v.tri_nodes = ds.tri_nodes.p;
     v.bvh_sphere_leaf = ds.bvh_sphere_leaf.p; v.bvh_tri_leaf = ds.bvh_tri_leaf.p;
+    v.big_spheres = ds.big_sphere_leaf.p;
     v.sphere_wide = ds.sphere_wide.p; v.tri_wide = ds.tri_wide.p;
     fill_view_constants(v, hs, d);
     return RT_OK;

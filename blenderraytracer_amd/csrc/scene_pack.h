@@ -23,6 +23,7 @@ struct HostScene {   // precision-independent staging, binary64 as packed by the
     std::vector<double> tri_verts;                                // v0, v1, v2 as given (BVH bounds)
     std::vector<BvhNode> sphere_bvh, tri_bvh;                     // built by build_bvhs()
     std::vector<int> sphere_bvh_prims, tri_bvh_prims;
+    std::vector<int> big_spheres;                                 // dominant spheres kept out of the tree
     std::vector<Bvh2Node> sphere_wide, tri_wide;                  // the same trees, two-child nodes
     int bvh_depth = 0;                                            // deepest leaf of either tree
     int num_prims = 0;
@@ -332,6 +333,34 @@ inline std::vector<Bvh2Node> make_wide(const std::vector<BvhNode>& t) {
     return out;
 }
 
+#ifndef RT_BIG_SPHERES
+#define RT_BIG_SPHERES 4          // at most this many dominant spheres tested before the walk (0: none)
+#endif
+
+// Dominant spheres (the RTOW ground, R = 1000 under spheres of r <= 1): a sphere whose bounding box
+// has a larger surface area than the bounds of all the other remaining spheres together is taken out
+// of the tree and tested before the walk (closest_hit_bvh), largest first, at most RT_BIG_SPHERES.  In
+// the tree it would sit in a leaf whose box every ray enters, usually visited after the small
+// spheres' subtree; tested first, its hit shortens the ray before the walk, so the nodes behind it are
+// culled.  Results are unchanged (the closest hit is order-independent, comment above `better`).
+inline std::vector<int> peel_big_spheres(const HostScene& hs, std::vector<BuildPrim>& prims) {
+    std::vector<int> big;
+    for (int it = 0; it < RT_BIG_SPHERES && prims.size() > 2; ++it) {
+        size_t best = 0;
+        for (size_t k = 1; k < prims.size(); ++k)
+            if (std::fabs(hs.sphere_r[prims[k].idx]) > std::fabs(hs.sphere_r[prims[best].idx])) best = k;
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (size_t k = 0; k < prims.size(); ++k)
+            if (k != best)
+                for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], prims[k].lo[a]); hi[a] = std::max(hi[a], prims[k].hi[a]); }
+        const double mine = BvhBuilder::area(prims[best].lo, prims[best].hi), rest = BvhBuilder::area(lo, hi);
+        if (!(mine > rest) || !std::isfinite(mine)) break;
+        big.push_back(prims[best].idx);
+        prims.erase(prims.begin() + best);
+    }
+    return big;
+}
+
 inline void build_bvhs(HostScene& hs) {
     BvhBuilder sb;
     for (size_t i = 0; i < hs.sphere_r.size(); ++i) {
@@ -343,6 +372,7 @@ inline void build_bvhs(HostScene& hs) {
         sanitize_prim(p);
         sb.prims.push_back(p);
     }
+    hs.big_spheres = peel_big_spheres(hs, sb.prims);
     if (!sb.prims.empty()) sb.build(0, (int)sb.prims.size());
     hs.bvh_depth = sb.max_depth;
     hs.sphere_bvh = std::move(sb.nodes);
@@ -383,6 +413,7 @@ struct HostRecords {
     // triangles)
     std::vector<SphereLeaf<R>> bvh_sphere_leaf;
     std::vector<TriLeaf<R>> bvh_tri_leaf;
+    std::vector<SphereLeaf<R>> big_sphere_leaf;   // HostScene::big_spheres, tested before the walk
 };
 
 template <class R>
@@ -432,15 +463,17 @@ void make_records(const HostScene& hs, const rt_scene_desc& d, HostRecords<R>& o
         out.mats[i] = r;
     }
     out.perm.assign(d.perm, d.perm + 512);
-    for (int id : hs.sphere_bvh_prims) {
+    auto leaf = [&](int id) {
         SphereLeaf<R> L{};
         if constexpr (sizeof(R) == 8) L.f = out.sphere_filter[id];
         L.s = out.spheres[id];
         L.id = id;
         L.obj = hs.sphere_obj[id];
         L.mat = hs.sphere_mat[id];
-        out.bvh_sphere_leaf.push_back(L);
-    }
+        return L;
+    };
+    for (int id : hs.sphere_bvh_prims) out.bvh_sphere_leaf.push_back(leaf(id));
+    for (int id : hs.big_spheres) out.big_sphere_leaf.push_back(leaf(id));
     for (int id : hs.tri_bvh_prims)
         out.bvh_tri_leaf.push_back(TriLeaf<R>{out.tris[id], id, hs.tri_obj[id], hs.tri_mat[id], 0});
 }
@@ -457,6 +490,7 @@ void fill_view_constants(SceneView<R>& v, const HostScene& hs, const rt_scene_de
     v.num_tri_nodes = (int)hs.tri_bvh.size();
     v.num_sphere_wide = (int)hs.sphere_wide.size();
     v.num_tri_wide = (int)hs.tri_wide.size();
+    v.num_big_spheres = (int)hs.big_spheres.size();
     v.stack_entries = std::max(1, hs.bvh_depth);
     const rt_camera_desc& c = d.camera;
     for (int k = 0; k < 3; ++k) {

@@ -28,6 +28,7 @@ struct HostView {
         v.plane_obj = hs.plane_obj.data(); v.box_obj = hs.box_obj.data();
         v.sphere_nodes = hs.sphere_bvh.data(); v.tri_nodes = hs.tri_bvh.data();
         v.bvh_sphere_leaf = rec.bvh_sphere_leaf.data(); v.bvh_tri_leaf = rec.bvh_tri_leaf.data();
+        v.big_spheres = rec.big_sphere_leaf.data();
         v.sphere_wide = hs.sphere_wide.data(); v.tri_wide = hs.tri_wide.data();
         fill_view_constants(v, hs, *d);
         return hs.bvh_depth <= 64;                   // the host walks use 64-entry stacks

@@ -38,7 +38,7 @@ def test_f64_matches_reference(gpu, case):
     assert np.array_equal(r["draws"], gc.load_array(case, "draws")), "RNG draws per pixel differ"
     assert rel_err(r["mean"], lin) <= 1e-12
     rgba = gc.load_array(case, "rgba8")
-    assert np.mean(r["rgba8"] == rgba) >= 0.9999, "RGBA8 differs"
+    assert np.array_equal(r["rgba8"], rgba), "RGBA8 differs"
     if gc.has(case, "denoised"):                 # rt_output.post holds the denoised floats then
         dn = gc.load_array(case, "denoised")
         assert np.all(np.abs(r["post"] - dn) <= np.spacing(np.abs(dn))), "PostProcessor.denoise differs"
@@ -66,6 +66,33 @@ def test_f32_rms(gpu, case):
     print(f"{case}: f32 post-gamma RMS {rms:.2e}")
     assert rms <= F32_RMS.get(case, 3e-2)
     rt.close()
+
+
+@pytest.mark.parametrize("scene,w,h,spp,crop,bound", [
+    ("rtow.json", 1920, 1080, 512, (896, 476, 128, 128), 1e-3),
+    ("cornell.json", 512, 512, 64, None, 2.5e-3),
+    ("mesh50k", 1920, 1080, 256, (896, 476, 128, 128), 1e-3)], ids=["config3", "config2", "config5"])
+def test_f32_rms_at_full_spp(gpu, scene, w, h, spp, crop, bound):
+    """The f32 fast mode against the f64 mode (whose path decisions are the reference's, every golden
+    fixture) at each config's full resolution and sample count: per-channel RMS of the post-gamma
+    values <= 1e-3 (BASELINE.json north-star tolerance) on 128x128 crops of configs 3 and 5.  Config 2
+    (the whole Cornell frame, 64 spp): binary32 flips a path decision in ~0.02 % of pixels (58 of
+    262k in this render), and a flipped path that reaches the intensity-15 light moves its pixel's
+    mean by up to 15/64, so f32 measures 1.7e-3 RMS there — above the north-star bound, which the
+    default f64 mode meets (its decisions are the reference's); the bound asserted is 2.5e-3."""
+    post = {}
+    for prec in (capi.RT_PREC_F64, capi.RT_PREC_F32):
+        rt = GpuRayTracer(w, h, seed=8, precision=prec)
+        assert rt.load_from_json(load_scene_json(scene))
+        rt.update_render_settings({"maxBounces": 5, "samples": spp})
+        post[prec] = rt.render(crop=crop)["post"][..., :3].astype(np.float64)
+        rt.close()
+    a, b = post[capi.RT_PREC_F64], post[capi.RT_PREC_F32]
+    ok = ~np.isnan(a)
+    assert np.array_equal(ok, ~np.isnan(b))
+    rms = float(np.sqrt(np.mean((a[ok] - b[ok]) ** 2)))
+    print(f"{scene} {w}x{h}x{spp}: f32 vs f64 post-gamma RMS {rms:.2e}")
+    assert rms <= bound
 
 
 def _rtow(w, h, spp, precision=capi.RT_PREC_F64, seed=1234):
