@@ -190,6 +190,29 @@ RT_HD void sphere_test_f64(const SceneView<R>& sc, V3<R> o, V3<R> d, R a, R tmin
 // |X - Y - (r2p - r^2) - delta| <= 27u Q, while r2p - r^2 + delta >= 2^-17 Q = 128u Q.  Hence
 // disc64 >= 0 (Y >= -2^-48 Q) implies X > 0: a rejected sphere (X < 0) is a sure binary64 miss.
 // NaN never rejects.  tests/test_sphere_filter.py checks this on adversarial near-tangent cases.
+// Approximate binary32 reciprocal / reciprocal square root (v_rcp_f32 / v_rsq_f32, <= 1 ulp) for the
+// conservative binary32 pre-tests only (sphere filter direction, BVH slab 1/d): their error bounds
+// (sphere_filter_bound, bvh_conservative_bound) carry margins of 4x and 16x over a correctly rounded
+// one, and a +-inf / NaN result behaves as before (clamped / never rejecting).  The correctly rounded
+// divisions they replace cost ~10 VALU each.  RT_FAST_RCP=0: correctly rounded (A/B).
+#ifndef RT_FAST_RCP
+#define RT_FAST_RCP 1
+#endif
+RT_HD float rt_rcp_approx(float x) {
+#if RT_FAST_RCP && defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+RT_HD float rt_rsqrt_approx(float x) {
+#if RT_FAST_RCP && defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rsqf(x);
+#else
+    return 1.0f / sqrtf(x);
+#endif
+}
+
 struct FilterRay { float ox, oy, oz, dx, dy, dz, delta; };
 
 template <class R>
@@ -197,7 +220,7 @@ RT_HD FilterRay make_filter_ray(V3<R> o, V3<R> d) {
     FilterRay f;
     f.ox = (float)o.x; f.oy = (float)o.y; f.oz = (float)o.z;
     const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
-    const float inv = 1.0f / sqrtf(dx * dx + dy * dy + dz * dz);
+    const float inv = rt_rsqrt_approx(dx * dx + dy * dy + dz * dz);
     f.dx = dx * inv; f.dy = dy * inv; f.dz = dz * inv;
     f.delta = (f.ox * f.ox + f.oy * f.oy + f.oz * f.oz) * (0x1p-16f * (1.0f + 0x1p-20f));
     return f;
@@ -360,7 +383,7 @@ RT_HD BvhRay make_bvh_ray(V3<R> o, V3<R> d) {
     for (int k = 0; k < 3; ++k) {
         r.olo[k] = of[k] + pad;      // (lo - olo) * inv and (hi - ohi) * inv widen the slab for both signs of d
         r.ohi[k] = of[k] - pad;
-        float inv = 1.0f / df[k];
+        float inv = rt_rcp_approx(df[k]);
         if (!(fabsf(inv) <= 0x1p126f)) inv = copysignf(0x1p126f, df[k]);
         r.inv[k] = inv;
         r.slo[k] = r.olo[k] * inv;

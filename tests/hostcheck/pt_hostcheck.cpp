@@ -236,3 +236,4 @@ extern "C" int ptc_work(const rt_scene_desc* d, const rt_settings* s, double* ou
 extern "C" void ptc_pow5(const double* x, double* out, long long n) {
     for (long long i = 0; i < n; ++i) out[i] = rt::pow5_rn<double>(x[i]);
 }
+

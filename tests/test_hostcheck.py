@@ -111,3 +111,4 @@ def test_pow5_correctly_rounded():
     diff = out != libm
     assert diff.mean() <= 1e-3
     assert np.all(np.abs(out[diff] - libm[diff]) <= np.spacing(np.abs(libm[diff])))
+
