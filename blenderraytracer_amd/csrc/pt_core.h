@@ -782,12 +782,13 @@ __host__ __device__ RT_COLD V3<R> background_procedural(const SceneView<R>& sc, 
     return ((((sky_c + glow_c) + gnd_c) + sun_c) + cl_c) * I;
 }
 
+// unit: normalize(d), computed by the caller (shade_segment shares it with the scatter of other lanes)
 template <class R>
-__host__ __device__ V3<R> background(const SceneView<R>& sc, V3<R> d) {
+__host__ __device__ V3<R> background(const SceneView<R>& sc, V3<R> d, V3<R> unit) {
     const R I = sc.sky_intensity;
     switch (sc.background) {
     case 0: {                                                                         // skyGradient
-        R t = (R)0.5 * (normalize(d).y + (R)1);
+        R t = (R)0.5 * (unit.y + (R)1);
         return (mk<R>(1, 1, 1) * ((R)1 - t) + mk<R>(0.5, 0.7, 1.0) * t) * I;
     }
     case 1:                                                                           // solid

@@ -91,21 +91,24 @@ RT_HD R pow5_rn(R x) {
 }
 
 // Scatter at a non-emissive hit (materials.js:20-83).  Returns false when Metal absorbs.
+// The three materials share their common steps so that a wave holding several of them runs each step
+// once (a branch runs for the union of its lanes): Lambertian and Metal draw one randomInUnitSphere
+// and nothing else (Metal's reflect draws nothing), so that rejection loop runs before the material
+// branch (RTOW +3.8 %), and the one normalize each material needs — Lambertian the unit-sphere point
+// `p`, Metal and Dielectric the ray direction — arrives as `unit`, computed by shade_segment together
+// with the missed rays' (skyGradient's) normalize (+1.6 %).
 template <class R>
-RT_HD bool scatter(const MatRec<R>& m, const Hit<R>& h, V3<R> d, Rng<R>& g, V3<R>& nd, V3<R>& att) {
-    if (m.type == 0) {                                                        // Lambertian :20-25
-        nd = h.n + normalize(random_in_unit_sphere(g));
+RT_HD bool scatter(const MatRec<R>& m, const Hit<R>& h, V3<R> unit, V3<R> p, Rng<R>& g, V3<R>& nd, V3<R>& att) {
+    if (m.type <= 1) {
         att = mk(m.albedo[0], m.albedo[1], m.albedo[2]);
-        return true;
-    }
-    if (m.type == 1) {                                                        // Metal :36-41
-        V3<R> refl = reflect(normalize(d), h.n);
-        nd = refl + random_in_unit_sphere(g) * m.rough;
-        att = mk(m.albedo[0], m.albedo[1], m.albedo[2]);
+        if (m.type == 0) {                                                    // Lambertian :20-25
+            nd = h.n + unit;
+            return true;
+        }
+        nd = reflect(unit, h.n) + p * m.rough;                                // Metal :36-41
         return dot(nd, h.n) > (R)0;
     }
     R ratio = h.front ? ((R)1 / m.ior) : m.ior;                               // Dielectric :51-83
-    V3<R> unit = normalize(d);
     R cos_t = js_min<R>(dot(unit * (R)-1, h.n), (R)1);
     R sin_t = sqrt((R)1 - cos_t * cos_t);
     bool reflect_it = ratio * sin_t > (R)1;
@@ -148,14 +151,24 @@ RT_HD bool shade_segment(const SceneView<R>& sc, const Closest<R>& c, V3<R>& o, 
                          Rng<R>& g, V3<R>& L) {
     bool done = true;
     L = mk<R>(0, 0, 0);
-    if (c.kind != HIT_NONE) {
-        const Hit<R> h = hit_record(sc, o, d, c);
-        const MatRec<R> m = sc.mats[h.mat];
+    const bool hit = c.kind != HIT_NONE;
+    Hit<R> h{};
+    MatRec<R> m{};
+    V3<R> p = mk<R>(0, 0, 0);
+    if (hit) {
+        h = hit_record(sc, o, d, c);
+        m = sc.mats[h.mat];
+        if (m.type <= 1) p = random_in_unit_sphere(g);                       // Lambertian / Metal's only draws
+    }
+    // one normalize for every lane (see scatter): Lambertian's p, else the ray direction (Metal,
+    // Dielectric, and a missed ray's skyGradient)
+    const V3<R> unit = normalize(hit && m.type == 0 ? p : d);
+    if (hit) {
         if (m.type == 3) {                                                    // Emissive (materials.js:87-96)
             L = mk(T.x * m.emit[0], T.y * m.emit[1], T.z * m.emit[2]);
         } else {
             V3<R> nd, att;
-            if (scatter(m, h, d, g, nd, att)) {
+            if (scatter(m, h, unit, p, g, nd, att)) {
                 T = mk(T.x * att.x, T.y * att.y, T.z * att.z);
                 o = h.p;
                 d = nd;
@@ -163,7 +176,7 @@ RT_HD bool shade_segment(const SceneView<R>& sc, const Closest<R>& c, V3<R>& o, 
             }
         }
     } else {
-        const V3<R> bg = background(sc, d);                                   // world.background(ray)
+        const V3<R> bg = background(sc, d, unit);                             // world.background(ray)
         L = mk(T.x * bg.x, T.y * bg.y, T.z * bg.z);
     }
     return done;
