@@ -144,7 +144,10 @@ struct BvhBuilder {
     std::vector<int> order;
     int max_depth = 0;                              // deepest leaf (root = 0)
 #ifndef RT_BVH_LEAF
-#define RT_BVH_LEAF 2             // measured: 1 / 2 / 4 / 8 within 3 % on RTOW, 2 best on mesh50k
+#define RT_BVH_LEAF 2             // triangles: measured 1 / 2 / 4 / 8 within 3 % on RTOW, 2 best on mesh50k
+#endif
+#ifndef RT_BVH_SPHERE_LEAF
+#define RT_BVH_SPHERE_LEAF 1      // spheres: 1 vs 2 vs 3 on RTOW (dominant sphere peeled): +0.9 % / 0 / -1.2 %
 #endif
 #ifndef RT_BVH_BINS
 #define RT_BVH_BINS 16
@@ -152,7 +155,7 @@ struct BvhBuilder {
 #ifndef RT_BVH_SWEEP
 #define RT_BVH_SWEEP 0            // 1: full-sweep SAH over all three axes instead of binned on the widest
 #endif
-    static constexpr int kLeafMax = RT_BVH_LEAF;   // primitives per leaf (<= 15)
+    int kLeafMax = RT_BVH_LEAF;                     // primitives per leaf (<= 15)
     static constexpr int kBins = RT_BVH_BINS;      // SAH bins
 
     static double area(const double* lo, const double* hi) {
@@ -161,7 +164,7 @@ struct BvhBuilder {
     }
 
     // levels a median-split subtree of `count` primitives needs below its root
-    static int median_levels(int count) {
+    int median_levels(int count) const {
         int l = 0;
         for (long long c = (count + kLeafMax - 1) / kLeafMax; c > 1; c = (c + 1) / 2) ++l;
         return l;
@@ -363,6 +366,7 @@ inline std::vector<int> peel_big_spheres(const HostScene& hs, std::vector<BuildP
 
 inline void build_bvhs(HostScene& hs) {
     BvhBuilder sb;
+    sb.kLeafMax = RT_BVH_SPHERE_LEAF;
     for (size_t i = 0; i < hs.sphere_r.size(); ++i) {
         const double* s = &hs.spheres[4 * i];
         const double r = std::fabs(hs.sphere_r[i]);       // negative radius: same sphere, inverted normal
