@@ -224,13 +224,15 @@ def node_end_to_end(cfg, args):
                     "Float32 readback"}
 
 
-def git_head():
-    try:
-        import subprocess
-        return subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
-                              timeout=10).stdout.strip() or None
-    except Exception:
-        return None
+def build_provenance():
+    """The commit / source digest librt_hip.so was built from (lib/build_info.json, written by the build)
+    and whether the sources in this tree still hash the same (the GPU box has no .git)."""
+    from blenderraytracer_amd import build as B
+    info = B.read_build_info() or {}
+    tree = B.source_digest()
+    return {"commit": info.get("commit"), "sources_modified_at_build": info.get("sources_modified"),
+            "library_source_digest": info.get("source_digest"), "tree_source_digest": tree,
+            "library_matches_tree": info.get("source_digest") == tree}
 
 
 def main():
@@ -332,7 +334,7 @@ def main():
                                  "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes over one "
                                            "frame run by this bench invocation (FETCH x2 per the gfx950 correction, "
                                            "KiB x1024) / this run's HIP-event trace-step time",
-                                 "commit": git_head()})
+                                 "commit": build_provenance()["commit"]})
                 sq = pmc["sq"]["total"]
                 f64 = sum(sq.get(f"SQ_INSTS_VALU_{k}_F64", 0.0) for k in ("ADD", "MUL", "FMA", "TRANS"))
                 slots = sq.get("SQ_INSTS_VALU", 0.0) + f64
@@ -376,6 +378,7 @@ def main():
             "cpu_baseline": cpu,
             "end_to_end": e2e,
             "end_to_end_node": e2e_node,
+            "build": build_provenance(),
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -6,6 +6,8 @@ Flags: -ffp-contract=off keeps every binary64 operation unfused, like JavaScript
 (NaN/Inf semantics are part of Box.hit and the JSON-solid background, SURVEY §7 hard part 1).
 The N-API addon (csrc/napi_addon.cpp, for the Node host) is built with --napi when Node headers exist.
 """
+import hashlib
+import json
 import os
 import shutil
 import subprocess
@@ -35,6 +37,45 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def source_digest():
+    """sha256 (16 hex digits) over the library's sources: csrc/ and include/, names and bytes."""
+    h = hashlib.sha256()
+    for d in (CSRC, os.path.join(REPO, "include")):
+        for f in sorted(os.listdir(d)):
+            p = os.path.join(d, f)
+            if os.path.isfile(p):
+                h.update(f.encode())
+                with open(p, "rb") as fh:
+                    h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def _git(*args):
+    try:
+        return subprocess.run(["git", "-C", REPO, *args], capture_output=True, text=True, timeout=10).stdout.strip()
+    except Exception:
+        return ""
+
+
+def write_build_info():
+    """lib/build_info.json: the commit and source digest librt_hip.so was built from (travels with the
+    library; bench.py reports it, so a profile names the sources it measured)."""
+    info = {"commit": _git("rev-parse", "--short", "HEAD") or None,
+            "sources_modified": bool(_git("status", "--porcelain", "--", CSRC, os.path.join(REPO, "include"))),
+            "source_digest": source_digest()}
+    with open(os.path.join(LIBDIR, "build_info.json"), "w") as f:
+        json.dump(info, f)
+    return info
+
+
+def read_build_info():
+    try:
+        with open(os.path.join(LIBDIR, "build_info.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
 def build_lib(force=False):
     os.makedirs(LIBDIR, exist_ok=True)
     target = os.path.join(LIBDIR, "librt_hip.so")
@@ -47,6 +88,7 @@ def build_lib(force=False):
         _run([HIPCC, *HIP_FLAGS, "-c", os.path.join(CSRC, src), "-o", obj])
         objs.append(obj)
     _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", target, *objs])
+    write_build_info()
     return target
 
 

@@ -74,3 +74,15 @@ def test_invalid_descriptor_rejected(lib):
     h = C.c_void_p()
     assert lib.rt_scene_create(C.byref(p.desc), 0, C.byref(h)) == -1
     assert lib.rt_scene_create(None, 0, C.byref(h)) == -1
+
+
+def test_library_records_the_sources_it_was_built_from(lib):
+    """lib/build_info.json (written by the build next to librt_hip.so) names the commit and the digest
+    of csrc/ + include/; bench.py reports both, so a profile names the sources it measured."""
+    from blenderraytracer_amd import build as B
+    info = B.read_build_info()
+    assert info is not None and len(info["source_digest"]) == 16
+    lib_mtime = os.path.getmtime(os.path.join(B.LIBDIR, "librt_hip.so"))
+    srcs = [os.path.join(d, f) for d in (B.CSRC, INCLUDE) for f in os.listdir(d)]
+    if all(os.path.getmtime(s) <= lib_mtime for s in srcs):     # library built after the last edit
+        assert info["source_digest"] == B.source_digest()
