@@ -82,8 +82,9 @@ def make_tracer(cfg, precision, seed, device, accel="auto"):
 
 
 # JS CPU baseline crops (side of the centred square crop, at full resolution, spp and depth): about
-# 10 s for one thread; the multi-thread run renders a crop twice the side
-JS_CROP = {"sample_scene": 64, "cornell": 48, "rtow": 32, "rtow4k": 24, "mesh50k": 4}
+# 10 s for one thread; the multi-thread run renders a crop twice the side.  Config 1 (the
+# reference's own CPU-runnable case) is timed on its whole 256x256 frame.
+JS_CROP = {"sample_scene": 256, "cornell": 48, "rtow": 32, "rtow4k": 24, "mesh50k": 4}
 
 
 def js_cpu_baseline(cfg_name, cfg, seed, workers, side):
