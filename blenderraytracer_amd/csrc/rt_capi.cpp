@@ -156,6 +156,7 @@ struct DeviceState {
     hipEvent_t scratch_ev = nullptr;   // recorded after every use of part / total (order_scratch)
     hipStream_t scratch_stream = nullptr;
     bool scratch_used = false;
+    hipEvent_t copy_ev = nullptr;      // a replica's batch sums copied out to the home device (merge_shards)
 
     int init(int dev, const HostScene& hs, const rt_scene_desc& d) {
         device = dev;
@@ -166,6 +167,7 @@ struct DeviceState {
         e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
         for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreate(&ev[k]);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&scratch_ev, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&copy_ev, hipEventDisableTiming);
         if (e != hipSuccess) return fail(RT_ERR_DEVICE, "stream/event create: %s", hipGetErrorString(e));
         return RT_OK;
     }
@@ -178,6 +180,7 @@ struct DeviceState {
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         if (scratch_ev) (void)hipEventDestroy(scratch_ev);
+        if (copy_ev) (void)hipEventDestroy(copy_ev);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -201,6 +204,14 @@ struct DescCopy {
 
 }  // namespace
 
+// A shard's staging buffers on the home device and the event that frees them (merge_shards).
+struct MergeSlot {
+    DevBuf<double> sum;
+    DevBuf<uint32_t> segs, draws;
+    hipEvent_t added = nullptr;     // recorded on the home stream after this slot's adds
+    bool pending = false;           // `added` has been recorded
+};
+
 struct rt_scene {
     DeviceState home;               // the device of rt_scene_create: epilogue, outputs, checkpoint
     std::vector<DeviceState*> replicas;   // rt_settings.devices[k] for k >= 1 (created on first use)
@@ -212,8 +223,8 @@ struct rt_scene {
     bool tri_bvh = false;           // the scene has a triangle BVH (pool chunk choice)
     double record_bytes = 0;
     hipEvent_t ev[2] = {};          // epilogue timing
-    DevBuf<double> mean, stage;     // stage: a shard's sums copied from its device
-    DevBuf<uint32_t> stage_u;
+    DevBuf<double> mean;
+    std::vector<MergeSlot> merge;   // per shard (index in the render's device list): its staging on home
     DevBuf<float> post, post_raw;   // post_raw: pre-denoise floatData
     DevBuf<uint8_t> rgba;
     std::atomic<int> cancel{0};
@@ -470,7 +481,11 @@ void rt_scene_destroy(rt_scene* sc) {
         }
     sc->home.release();
     (void)hipSetDevice(sc->home.device);
-    sc->mean.release(); sc->stage.release(); sc->stage_u.release(); sc->post.release(); sc->post_raw.release();
+    sc->mean.release(); sc->post.release(); sc->post_raw.release();
+    for (MergeSlot& m : sc->merge) {
+        m.sum.release(); m.segs.release(); m.draws.release();
+        if (m.added) (void)hipEventDestroy(m.added);
+    }
     sc->rgba.release();
     for (auto& e : sc->ev)
         if (e) (void)hipEventDestroy(e);
@@ -495,32 +510,41 @@ void shard_range(int b, int e, int k, int n, int& sb, int& se) {
 }
 
 // Adds the replicas' sums (and counters) of the batch just traced into the home device's, in shard
-// order (peer copies over xGMI into a staging buffer on the home device, then dst += stage), and zeroes
-// the replicas' buffers for the next batch.  Merging after every batch keeps the running sums on the
-// home device exactly what a checkpoint saves, so a resumed render is bit-identical.
+// order, without a host wait: each replica copies its batch sums over xGMI into its own staging slot on
+// the home device from its own stream (the copies of all replicas run at once, one link each) and then
+// zeroes them for its next batch; the home stream waits for each copy and adds the slots in shard
+// order, then records that the slot is free (the replica's next copy waits for that).  The home
+// device's own trace of the next batch follows the adds on its stream, so the running sums see the same
+// sequence of additions as a merge after every batch done synchronously: a checkpoint holds exactly
+// the merged batches and a resumed render is bit-identical.
 int merge_shards(rt_scene* sc, const std::vector<DeviceState*>& states, size_t n, bool segs, bool draws) {
     DeviceState& h = sc->home;
-    for (DeviceState* ds : states) {
+    if (sc->merge.size() < states.size()) sc->merge.resize(states.size());
+    for (size_t k = 0; k < states.size(); ++k) {
+        DeviceState* ds = states[k];
         if (ds == &h) continue;
-        HIP_TRY(hipSetDevice(ds->device));
-        HIP_TRY(hipStreamSynchronize(ds->stream));
+        MergeSlot& m = sc->merge[k];
         HIP_TRY(hipSetDevice(h.device));
-        HIP_TRY(sc->stage.ensure(3 * n));
-        HIP_TRY(hipMemcpyPeerAsync(sc->stage.p, h.device, ds->sum.p, ds->device, 3 * n * sizeof(double), h.stream));
-        HIP_TRY(launch_add<double>(h.sum.p, sc->stage.p, 3 * n, h.stream));
-        for (int k = 0; k < 2; ++k) {
-            if (!(k == 0 ? segs : draws)) continue;
-            HIP_TRY(sc->stage_u.ensure(n));
-            HIP_TRY(hipMemcpyPeerAsync(sc->stage_u.p, h.device, (k == 0 ? ds->segs : ds->draws).p, ds->device,
-                                       n * sizeof(uint32_t), h.stream));
-            HIP_TRY(launch_add<uint32_t>((k == 0 ? h.segs : h.draws).p, sc->stage_u.p, n, h.stream));
-        }
-        HIP_TRY(hipStreamSynchronize(h.stream));     // the staging buffers are reused by the next shard
+        HIP_TRY(m.sum.ensure(3 * n));
+        if (segs) HIP_TRY(m.segs.ensure(n));
+        if (draws) HIP_TRY(m.draws.ensure(n));
+        if (!m.added) HIP_TRY(hipEventCreateWithFlags(&m.added, hipEventDisableTiming));
         HIP_TRY(hipSetDevice(ds->device));
+        if (m.pending) HIP_TRY(hipStreamWaitEvent(ds->stream, m.added, 0));    // the slot's last adds are done
+        HIP_TRY(hipMemcpyPeerAsync(m.sum.p, h.device, ds->sum.p, ds->device, 3 * n * sizeof(double), ds->stream));
+        if (segs) HIP_TRY(hipMemcpyPeerAsync(m.segs.p, h.device, ds->segs.p, ds->device, n * sizeof(uint32_t), ds->stream));
+        if (draws) HIP_TRY(hipMemcpyPeerAsync(m.draws.p, h.device, ds->draws.p, ds->device, n * sizeof(uint32_t), ds->stream));
+        HIP_TRY(hipEventRecord(ds->copy_ev, ds->stream));
         HIP_TRY(hipMemsetAsync(ds->sum.p, 0, 3 * n * sizeof(double), ds->stream));
         if (segs) HIP_TRY(hipMemsetAsync(ds->segs.p, 0, n * sizeof(uint32_t), ds->stream));
         if (draws) HIP_TRY(hipMemsetAsync(ds->draws.p, 0, n * sizeof(uint32_t), ds->stream));
         HIP_TRY(hipSetDevice(h.device));
+        HIP_TRY(hipStreamWaitEvent(h.stream, ds->copy_ev, 0));
+        HIP_TRY(launch_add<double>(h.sum.p, m.sum.p, 3 * n, h.stream));
+        if (segs) HIP_TRY(launch_add<uint32_t>(h.segs.p, m.segs.p, n, h.stream));
+        if (draws) HIP_TRY(launch_add<uint32_t>(h.draws.p, m.draws.p, n, h.stream));
+        HIP_TRY(hipEventRecord(m.added, h.stream));
+        m.pending = true;
     }
     return RT_OK;
 }
@@ -631,9 +655,10 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         HIP_TRY(hipStreamSynchronize(ds->stream));
         for (int k = 0; k < kTotalSlots; ++k) totals[k] += t[k];
     }
-    if (status != RT_OK) return status;
     DeviceState& h = sc->home;
     HIP_TRY(hipSetDevice(h.device));
+    HIP_TRY(hipStreamSynchronize(h.stream));          // the merges of the last batch (checkpoint state)
+    if (status != RT_OK) return status;
     const bool want_mean = out && out->mean, want_post = out && out->post, want_rgba = out && out->rgba8;
     if (want_mean) HIP_TRY(sc->mean.ensure(3 * n));
     if (want_post) HIP_TRY(sc->post.ensure(4 * n));
