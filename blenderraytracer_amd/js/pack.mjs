@@ -47,8 +47,14 @@ function backgroundOf(world) {
     throw new Error('unsupported world.background');
 }
 
+// (indexed stores, no temporary array: packScene runs on every render() to detect scene changes, and
+// a 50k-triangle mesh is 600k values)
 function triangleRecord(t, out, k) {
-    out.set([t.v0.x, t.v0.y, t.v0.z, t.v1.x, t.v1.y, t.v1.z, t.v2.x, t.v2.y, t.v2.z, t.normal.x, t.normal.y, t.normal.z], 12 * k);
+    const b = 12 * k, v0 = t.v0, v1 = t.v1, v2 = t.v2, n = t.normal;
+    out[b] = v0.x; out[b + 1] = v0.y; out[b + 2] = v0.z;
+    out[b + 3] = v1.x; out[b + 4] = v1.y; out[b + 5] = v1.z;
+    out[b + 6] = v2.x; out[b + 7] = v2.y; out[b + 8] = v2.z;
+    out[b + 9] = n.x; out[b + 10] = n.y; out[b + 11] = n.z;
 }
 
 export function packScene(world, camera) {
@@ -61,48 +67,56 @@ export function packScene(world, camera) {
     let ntri = 0;
     for (const o of world.objects) if (o.triangles) ntri += o.triangles.length; else if (o.v0) ntri += 1;
     const tris = new Float64Array(Math.max(1, ntri) * 12);
+    // records through typed-array views (little-endian hosts, as the C ABI's x86-64 / aarch64 peers):
+    // plain indexed stores, no DataView calls or temporaries
     const objects = new ArrayBuffer(OBJECT_BYTES * world.objects.length);
-    const ov = new DataView(objects);
+    const oi = new Int32Array(objects), of = new Float64Array(objects);
     let k = 0;
-    world.objects.forEach((o, i) => {
-        const base = i * OBJECT_BYTES;
-        const g = (vals) => vals.forEach((v, j) => ov.setFloat64(base + 16 + 8 * j, v, true));
+    const objs = world.objects;
+    for (let i = 0; i < objs.length; i++) {
+        const o = objs[i];
+        const gi = i * (OBJECT_BYTES / 8) + 2;                    // g[0] at byte 16
+        const g = (a, b, c, d, e, f) => {
+            of[gi] = a; of[gi + 1] = b; of[gi + 2] = c; of[gi + 3] = d;
+            if (e !== undefined) { of[gi + 4] = e; of[gi + 5] = f; }
+        };
         let type, mat, first = 0, count = 0;
         if (o.triangles) {                                            // TriangleMesh
             type = OBJ.mesh;
             first = k; count = o.triangles.length;
             mat = count ? matOf(o.triangles[0].material) : matOf(o.material || { albedo: { x: 0, y: 0, z: 0 } });
-            for (const t of o.triangles) {
-                if (t.material !== o.triangles[0].material) throw new Error('mesh triangles with different materials');
+            const ts = o.triangles, m0 = count ? ts[0].material : null;
+            for (let j = 0; j < count; j++) {
+                const t = ts[j];
+                if (t.material !== m0) throw new Error('mesh triangles with different materials');
                 triangleRecord(t, tris, k++);
             }
         } else if (o.v0) {                                            // Triangle
             type = OBJ.triangle; mat = matOf(o.material); first = k; count = 1;
             triangleRecord(o, tris, k++);
         } else if (o.center !== undefined && o.radius !== undefined) {
-            type = OBJ.sphere; mat = matOf(o.material); g([o.center.x, o.center.y, o.center.z, o.radius]);
+            type = OBJ.sphere; mat = matOf(o.material); g(o.center.x, o.center.y, o.center.z, o.radius);
         } else if (o.point !== undefined && o.normal !== undefined) {
-            type = OBJ.plane; mat = matOf(o.material); g([o.point.x, o.point.y, o.point.z, o.normal.x, o.normal.y, o.normal.z]);
+            type = OBJ.plane; mat = matOf(o.material); g(o.point.x, o.point.y, o.point.z, o.normal.x, o.normal.y, o.normal.z);
         } else if (o.min !== undefined && o.max !== undefined) {
-            type = OBJ.box; mat = matOf(o.material); g([o.min.x, o.min.y, o.min.z, o.max.x, o.max.y, o.max.z]);
+            type = OBJ.box; mat = matOf(o.material); g(o.min.x, o.min.y, o.min.z, o.max.x, o.max.y, o.max.z);
         } else {
             throw new Error(`world.objects[${i}]: unsupported object`);
         }
-        ov.setInt32(base, type, true);
-        ov.setInt32(base + 4, mat, true);
-        ov.setInt32(base + 8, first, true);
-        ov.setInt32(base + 12, count, true);
-    });
+        const ii = i * (OBJECT_BYTES / 4);
+        oi[ii] = type; oi[ii + 1] = mat; oi[ii + 2] = first; oi[ii + 3] = count;
+    }
     const materials = new ArrayBuffer(MATERIAL_BYTES * Math.max(1, mats.length));
-    const mv = new DataView(materials);
-    mats.forEach((m, i) => {
-        const b = i * MATERIAL_BYTES;
-        mv.setInt32(b, m.type, true);
-        (m.albedo || [0, 0, 0]).forEach((v, j) => mv.setFloat64(b + 8 + 8 * j, v, true));
-        mv.setFloat64(b + 32, m.roughness || 0, true);
-        mv.setFloat64(b + 40, m.ior || 0, true);
-        (m.emit || [0, 0, 0]).forEach((v, j) => mv.setFloat64(b + 48 + 8 * j, v, true));
-    });
+    const mi = new Int32Array(materials), mf = new Float64Array(materials);
+    for (let i = 0; i < mats.length; i++) {
+        const m = mats[i], b = i * (MATERIAL_BYTES / 8);
+        mi[2 * b] = m.type;
+        const al = m.albedo || [0, 0, 0], em = m.emit || [0, 0, 0];
+        mf[b + 1] = al[0]; mf[b + 2] = al[1]; mf[b + 3] = al[2];
+        mf[b + 4] = m.roughness || 0;
+        mf[b + 5] = m.ior || 0;
+        mf[b + 6] = em[0]; mf[b + 7] = em[1]; mf[b + 8] = em[2];
+    }
     const c = camera;
     const cam = new Float64Array(22);
     [c.origin, c.lowerLeftCorner, c.horizontal, c.vertical, c.u, c.v, c.w].forEach((v, j) => cam.set([v.x, v.y, v.z], 3 * j));
