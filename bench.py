@@ -221,8 +221,8 @@ def node_end_to_end(cfg, args):
     return {"value": round(out["value"], 3), "unit": "Msamples/s", "wall_ms": round(out["wall_ms"], 3),
             "first_call_ms": round(out["first_call_ms"], 3), "kernel_ms": out["kernel_ms"],
             "what": "GpuRayTracer.render() from Node (the installGpuRender path): scene resident from the first call "
-                    "(first_call_ms includes its upload and BVH build), pack + compare, trace, epilogue, RGBA8 + "
-                    "Float32 readback"}
+                    "(first_call_ms includes its upload and BVH build), pack + compare, trace, epilogue, RGBA8 "
+                    "readback into imageData (what the reference's render() produces)"}
 
 
 def build_provenance():

@@ -3,7 +3,7 @@
 // The JS host (blenderraytracer_amd/js/gpu-ray-tracer.mjs) keeps the reference's RayTracer surface
 // and calls into this addon for the part under RayTracer.render (js/ray-tracer.js:166-281):
 //   createScene(desc, device)          -> External   (rt_scene_create: scene copied into HBM)
-//   render(scene, settings, progress?) -> Promise<{mean, post, rgba8, segments?, draws?, stats}>
+//   render(scene, settings, progress?) -> Promise<{mean?, post?, rgba8, segments?, draws?, stats}>
 //                                         (rt_render on a libuv worker thread: the event loop stays live)
 //   cancel(scene)                      -> rt_cancel (polled between sample batches)
 //   destroyScene(scene), deviceCount(), abiVersion()
@@ -186,7 +186,7 @@ struct RenderJob {
     rt_scene* scene = nullptr;
     rt_settings st{};
     size_t n = 0;
-    bool want_mean = false, want_counts = false;
+    bool want_mean = false, want_counts = false, want_post = true;
     // outputs live in JS ArrayBuffers created on the main thread before the work is queued (kept alive
     // by references, not visible to JS until the promise resolves): rt_render copies the frames from
     // HBM straight into them, with no staging vectors and no copy into the result.  settings.outRgba8
@@ -275,7 +275,8 @@ void complete(napi_env env, napi_status, void* data) {
     } else {
         napi_value res, stats, v;
         napi_create_object(env, &res);
-        napi_set_named_property(env, res, "post", out_array(env, job, RenderJob::OUT_POST, napi_float32_array, job->n * 4));
+        if (job->want_post)
+            napi_set_named_property(env, res, "post", out_array(env, job, RenderJob::OUT_POST, napi_float32_array, job->n * 4));
         napi_set_named_property(env, res, "rgba8", out_array(env, job, RenderJob::OUT_RGBA, napi_uint8_clamped_array, job->n * 4));
         if (job->want_mean) napi_set_named_property(env, res, "mean", out_array(env, job, RenderJob::OUT_MEAN, napi_float64_array, job->n * 3));
         if (job->want_counts) {
@@ -347,6 +348,7 @@ napi_value render(napi_env env, napi_callback_info info) {
     st.device_count = nd;
     job->want_mean = get_num(env, s, "wantMean", 0) != 0;
     job->want_counts = get_num(env, s, "wantCounts", 0) != 0;
+    job->want_post = get_num(env, s, "wantPost", 1) != 0;      // the post-gamma Float32 frame (default on)
     const int cw = st.crop_w > 0 ? st.crop_w : st.width, ch = st.crop_h > 0 ? st.crop_h : st.height;
     if (cw <= 0 || ch <= 0) {
         delete job;
@@ -363,8 +365,9 @@ napi_value render(napi_env env, napi_callback_info info) {
         job->resume.assign(static_cast<double*>(rs), static_cast<double*>(rs) + job->n * 3);
         job->resume_done = (int32_t)get_num(env, s, "resumeSamplesDone", 0);
     }
-    // output buffers (see RenderJob): post always, RGBA8 into settings.outRgba8 when it is the frame's size
-    bool ok = make_out(env, job, RenderJob::OUT_POST, job->n * 4 * sizeof(float));
+    // output buffers (see RenderJob): post unless settings.wantPost is 0, RGBA8 into settings.outRgba8
+    // when it is the frame's size
+    bool ok = !job->want_post || make_out(env, job, RenderJob::OUT_POST, job->n * 4 * sizeof(float));
     void* rgba_p = nullptr;
     size_t rgba_bytes = 0;
     napi_value rgba_v;

@@ -52,6 +52,8 @@ export function settingsOf(rt, opts = {}) {
         cropX0: opts.crop ? opts.crop[0] : 0, cropY0: opts.crop ? opts.crop[1] : 0,
         cropW: opts.crop ? opts.crop[2] : 0, cropH: opts.crop ? opts.crop[3] : 0,
         wantMean: opts.wantMean ? 1 : 0, wantCounts: opts.wantCounts ? 1 : 0,
+        // the post-gamma Float32 frame: render() keeps it (this.floatData) only on request
+        wantPost: opts.wantPost === false ? 0 : 1,
         // PostProcessor.denoise weights, evaluated with V8's Math.exp exactly as post-processor.js:55 does
         denoise: rt.denoising ? 1 : 0,
         denoiseW1: Math.exp(-(1) / (2 * rt.denoiseStrength * rt.denoiseStrength)),
@@ -115,15 +117,16 @@ export async function gpuRender(rt, onProgress, opts = {}) {
 function blit(rt, res) {
     // ray-tracer.js:215-276: RGBA8 top-down row-major, alpha 255, denoised when rt.denoising (all on the GPU)
     if (res.rgba8 !== rt.imageData.data) rt.imageData.data.set(res.rgba8);
-    rt.floatData = res.post;
+    if (res.post) rt.floatData = res.post;                         // opts.keepFloatData
     if (rt.ctx && rt.ctx.putImageData) rt.ctx.putImageData(rt.imageData, 0, 0);
 }
 
 // Option 1: swap the render() of a reference RayTracer instance for the GPU path.
-// opts: {seed, precision: 'f64'|'f32', accel, batchSamples, device, devices: [HIP ordinals]}
+// opts: {seed, precision: 'f64'|'f32', accel, batchSamples, device, devices: [HIP ordinals],
+//        keepFloatData: also read back the post-gamma Float32 frame into this.floatData}
 export function installGpuRender(rayTracer, opts = {}) {
     rayTracer.render = async function render(onProgress) {
-        const res = await gpuRender(this, onProgress, { ...opts, intoImageData: true });
+        const res = await gpuRender(this, onProgress, { ...opts, intoImageData: true, wantPost: !!opts.keepFloatData });
         if (!res) return;
         blit(this, res);
         this.lastStats = res.stats;
@@ -186,7 +189,7 @@ export class GpuRayTracer {
     }
 
     async render(onProgress) {
-        const res = await gpuRender(this, onProgress, { ...this.opts, intoImageData: true });
+        const res = await gpuRender(this, onProgress, { ...this.opts, intoImageData: true, wantPost: !!this.opts.keepFloatData });
         if (!res) return;
         blit(this, res);
         this.lastStats = res.stats;
@@ -196,7 +199,8 @@ export class GpuRayTracer {
     // Continue the last cancelled render (window.renderCancelled) from its checkpoint.
     async resume(onProgress) {
         if (!this.checkpointState) return this.render(onProgress);
-        const res = await gpuRender(this, onProgress, { ...this.opts, resume: this.checkpointState, intoImageData: true });
+        const res = await gpuRender(this, onProgress, { ...this.opts, resume: this.checkpointState, intoImageData: true,
+                                                        wantPost: !!this.opts.keepFloatData });
         if (!res) return;
         this.checkpointState = null;
         blit(this, res);

@@ -1,7 +1,8 @@
 // Node end-to-end timing of the drop-in (bench.py's end_to_end_node): GpuRayTracer.render() — the same
 // gpuRender() that installGpuRender() puts on the reference's RayTracer — on a bench workload.
 // The first render() uploads the scene and builds the BVHs; the timed second one reuses the resident
-// scene (packScene + byte compare), traces, runs the epilogue and copies RGBA8 + Float32 frames back.
+// scene (packScene + byte compare), traces, runs the epilogue and copies the RGBA8 frame into
+// imageData (the reference's render() output; the Float32 frame only with keepFloatData).
 //   node scripts/node_e2e.mjs '{"scene": path, "width", "height", "spp", "depth", "seed", "precision"}'
 import fs from 'fs';
 import { GpuRayTracer } from '../blenderraytracer_amd/js/gpu-ray-tracer.mjs';
