@@ -195,12 +195,15 @@ extern "C" long long ptc_bvh_check(const rt_scene_desc* d, long long n, unsigned
     return bad;
 }
 
-// BVH shape: deepest leaf of the binary trees and their two-child node count
-extern "C" int ptc_bvh_info(const rt_scene_desc* d, int* depth, int* nodes2) {
+// BVH shape: deepest leaf of the binary trees, their two-child node count, and the dominant spheres
+// tested before the walk (their sphere indices into big[0..*nbig), at most 8 written)
+extern "C" int ptc_bvh_info(const rt_scene_desc* d, int* depth, int* nodes2, int* nbig, int* big) {
     HostView<double> hv;
     hv.init(d);
     *depth = hv.hs.bvh_depth;
     *nodes2 = (int)(hv.hs.sphere_wide.size() + hv.hs.tri_wide.size());
+    *nbig = (int)hv.hs.big_spheres.size();
+    for (int k = 0; k < *nbig && k < 8; ++k) big[k] = hv.hs.big_spheres[k];
     return 0;
 }
 

@@ -32,7 +32,7 @@ def _bind(L):
                              C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.ptc_bvh_check.argtypes = [C.POINTER(capi.SceneDesc), C.c_longlong, C.c_uint, C.POINTER(C.c_longlong)]
     L.ptc_bvh_check.restype = C.c_longlong
-    L.ptc_bvh_info.argtypes = [C.POINTER(capi.SceneDesc)] + [C.POINTER(C.c_int)] * 2
+    L.ptc_bvh_info.argtypes = [C.POINTER(capi.SceneDesc)] + [C.POINTER(C.c_int)] * 4
     return L
 
 
@@ -48,9 +48,14 @@ def lib(defines=()):
 
 def bvh_info(packed, L=None):
     """(deepest leaf of the binary trees, two-child nodes)"""
-    v = [C.c_int() for _ in range(2)]
-    (L or lib()).ptc_bvh_info(C.byref(packed.desc), *[C.byref(x) for x in v])
-    return tuple(x.value for x in v)
+    return bvh_shape(packed, L)[:2]
+
+
+def bvh_shape(packed, L=None):
+    """(deepest leaf, two-child nodes, sphere indices of the dominant spheres tested before the walk)"""
+    depth, nodes2, nbig, big = C.c_int(), C.c_int(), C.c_int(), (C.c_int * 8)()
+    (L or lib()).ptc_bvh_info(C.byref(packed.desc), C.byref(depth), C.byref(nodes2), C.byref(nbig), big)
+    return depth.value, nodes2.value, list(big[:nbig.value])
 
 
 def bvh_check(packed, n, seed):

@@ -56,6 +56,17 @@ if (cmd === 'pack') {
     const seen = [];
     await rt.render((f) => seen.push(f));
     summary._render = { progress: seen, nonzero: rt.imageData.data.some((v, i) => i % 4 !== 3 && v > 0) };
+    // render() reads back only the RGBA8 frame; the post-gamma Float32 frame with keepFloatData
+    {
+        const { rt: kept } = tracerFor('sample_scene_aa_none', { keepFloatData: true });
+        await kept.render();
+        const ref = await kept.renderBuffers({});
+        summary._floatData = {
+            absentByDefault: rt.floatData === undefined,
+            kept: !!kept.floatData && kept.floatData.length === ref.post.length && kept.floatData.every((v, i) => Object.is(v, ref.post[i])),
+            rgbaEqual: rt.imageData.data.every((v, i) => v === kept.imageData.data[i]),
+        };
+    }
     // progressive: window.renderCancelled mid-frame, then resume() from the checkpoint
     {
         const { rt: full } = tracerFor('kitchen_sink', { batchSamples: 2 });   // same sample batches

@@ -91,6 +91,22 @@ def test_bvh_depth_cap_forces_median_splits():
     assert capped.ptc_bvh_check(C.byref(rt.packed().desc), 50_000, 7, C.byref(hits)) == 0 and hits.value > 5000
 
 
+def test_dominant_spheres_rtow():
+    """scene_pack.h peel_big_spheres: on RTOW the spheres above 1/64 of the other spheres' box area are
+    the R = 1000 ground and the three r = 1 spheres, taken out of the tree largest first (tested before
+    the walk); every other sphere stays in the tree.  The closest hit is unchanged (the BVH-vs-World
+    checks above run on the same build)."""
+    from blenderraytracer_amd.renderer import GpuRayTracer
+    from blenderraytracer_amd.scene import load_scene_json
+    rt = GpuRayTracer(64, 36, seed=3)
+    assert rt.load_from_json(load_scene_json("rtow.json"))
+    p = rt.packed()
+    radii = [o.g[3] for o in p.objects if o.type == 0]
+    big = hb.bvh_shape(p)[2]
+    assert [abs(radii[i]) for i in big] == [1000.0, 1.0, 1.0, 1.0]
+    assert max(abs(r) for i, r in enumerate(radii) if i not in big) < 1.0
+
+
 def test_pow5_correctly_rounded():
     """pow5_rn (Schlick's Math.pow(1 - cosine, 5) in the kernel, pt_path.h) is the correctly rounded
     x^5 (exact rational arithmetic) on 100k arguments 1 - c over the dielectric's range of cosines,

@@ -155,6 +155,7 @@ def test_js_gpu_render_matches_reference(gpu):
             assert np.mean(ld("rgba8", np.uint8).reshape(ch, cw, 4) == gc.load_array(name, "rgba8")) >= 0.9999
         r = summary["_render"]
         assert r["progress"][-1] == 1.0 and r["nonzero"]
+        assert summary["_floatData"] == {"absentByDefault": True, "kept": True, "rgbaEqual": True}
         # window.renderCancelled set in the 2nd of 4 progress callbacks, then GpuRayTracer.resume():
         # the same image.  The callbacks reach the JS thread asynchronously, so a fast enough GPU
         # finishes all batches before the cancel lands (samplesDone 8, resume then has nothing left);
