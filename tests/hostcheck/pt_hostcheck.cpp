@@ -132,6 +132,44 @@ extern "C" int ptc_sphere_filter_check(long long n, unsigned seed, double* max_r
     return (int)violations;
 }
 
+// Away-rejection (sphere_candidate's `away`): rays leaving a sphere's surface — the origin is the hit
+// point o + t d of a previous ray computed in binary64, the new direction random (outward, inward,
+// grazing) — and random rays elsewhere.  Returns the number of cases where the rejection changes the
+// decision or t of the full test; *taken counts the cases it rejected early.
+extern "C" long long ptc_away_check(long long n, unsigned seed, long long* taken) {
+    std::mt19937_64 gen(seed);
+    std::uniform_real_distribution<double> U(-1.0, 1.0);
+    long long bad = 0, early = 0;
+    for (long long it = 0; it < n; ++it) {
+        const double scale = std::pow(10.0, 4.0 * U(gen));
+        const double r = (it % 3 == 0 ? 1000.0 : std::fabs(U(gen)) + 1e-3) * scale * (U(gen) < 0 ? -1 : 1);
+        const SphereRec<double> s{U(gen) * scale, U(gen) * scale, U(gen) * scale, r * r};
+        V3<double> o, d{U(gen), U(gen), U(gen)};
+        if (it & 1) {                       // a hit point on the sphere from a ray aimed at it
+            const V3<double> o0{s.cx + 3 * std::fabs(r) * U(gen), s.cy + 3 * std::fabs(r) * U(gen), s.cz + 3 * std::fabs(r) * U(gen)};
+            const V3<double> d0{s.cx - o0.x + 0.5 * r * U(gen), s.cy - o0.y + 0.5 * r * U(gen), s.cz - o0.z + 0.5 * r * U(gen)};
+            double t0;
+            if (!sphere_candidate(s, o0, d0, dot(d0, d0), 0.001, t0)) continue;
+            o = o0 + d0 * t0;
+            if (it & 2) {                   // nearly tangent outgoing directions
+                const V3<double> nrm = (o - mk(s.cx, s.cy, s.cz)) * (1.0 / r);
+                d = d - nrm * dot(d, nrm) + nrm * (1e-9 * U(gen));
+            }
+        } else {
+            o = V3<double>{s.cx + 4 * std::fabs(r) * U(gen), s.cy + 4 * std::fabs(r) * U(gen), s.cz + 4 * std::fabs(r) * U(gen)};
+        }
+        const double a = dot(d, d);
+        double ta = 0, tb = 0;
+        const bool ha = sphere_candidate(s, o, d, a, 0.001, ta, true);
+        const bool hb = sphere_candidate(s, o, d, a, 0.001, tb, false);
+        if (ha != hb || (ha && ta != tb)) ++bad;
+        const V3<double> oc = o - mk(s.cx, s.cy, s.cz);
+        early += (oc.x * oc.x + oc.y * oc.y + oc.z * oc.z) - s.r2 >= 0 && oc.x * d.x + oc.y * d.y + oc.z * d.z >= 0;
+    }
+    *taken = early;
+    return bad;
+}
+
 // BVH stress: n random rays per scene, closest_hit (World order) vs closest_hit_bvh.  Rays start at
 // random points and aim at random primitives' surfaces (near-tangent for spheres, near edges and
 // vertices for triangles) to exercise the conservative node bounds.  Returns the number of rays

@@ -33,6 +33,8 @@ def _bind(L):
     L.ptc_bvh_check.argtypes = [C.POINTER(capi.SceneDesc), C.c_longlong, C.c_uint, C.POINTER(C.c_longlong)]
     L.ptc_bvh_check.restype = C.c_longlong
     L.ptc_bvh_info.argtypes = [C.POINTER(capi.SceneDesc)] + [C.POINTER(C.c_int)] * 4
+    L.ptc_away_check.argtypes = [C.c_longlong, C.c_uint, C.POINTER(C.c_longlong)]
+    L.ptc_away_check.restype = C.c_longlong
     return L
 
 

@@ -107,6 +107,17 @@ def test_dominant_spheres_rtow():
     assert max(abs(r) for i, r in enumerate(radii) if i not in big) < 1.0
 
 
+def test_away_rejection_is_exact():
+    """sphere_candidate's early rejection (origin outside or on the sphere, moving away) never changes
+    the full binary64 test's decision or t: 2 M rays, half of them leaving a sphere from a binary64
+    hit point (a quarter nearly tangent), radii from 1e-3 to 1e7 including the RTOW ground's R = 1000
+    and negative radii."""
+    import ctypes as C
+    taken = C.c_longlong()
+    assert hb.lib().ptc_away_check(2_000_000, 11, C.byref(taken)) == 0
+    assert taken.value > 300_000          # the shortcut is exercised
+
+
 def test_pow5_correctly_rounded():
     """pow5_rn (Schlick's Math.pow(1 - cosine, 5) in the kernel, pt_path.h) is the correctly rounded
     x^5 (exact rational arithmetic) on 100k arguments 1 - c over the dielectric's range of cosines,
