@@ -67,3 +67,15 @@ def tracer_for(case, precision=capi.RT_PREC_F64, device=0):
         rt.update_background(c["background_in"]["type"], c["background_in"]["intensity"])
     assert (rt.width, rt.height) == (c["width"], c["height"])
     return rt, c
+
+
+def ensure_mesh50k_file():
+    """scenes/mesh50k.json is git-ignored: the Node tools read it from disk, so write it once."""
+    from blenderraytracer_amd.scene import SCENES_DIR
+    p = os.path.join(SCENES_DIR, "mesh50k.json")
+    if not os.path.exists(p) or os.path.getsize(p) == 0:
+        data = load_scene_json("mesh50k")  # generated before the file exists (no empty-file race)
+        tmp = p + f".tmp{os.getpid()}"
+        with open(tmp, "w") as f:
+            json.dump(data, f)
+        os.replace(tmp, p)

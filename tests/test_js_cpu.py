@@ -22,7 +22,7 @@ pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
 
 @pytest.fixture(scope="module")
 def js_outputs(tmp_path_factory):
-    load_scene_json("mesh50k")                     # generated on demand (git-ignored)
+    gc.ensure_mesh50k_file()                       # generated on demand (git-ignored)
     out = tmp_path_factory.mktemp("jscpu")
     subprocess.run([NODE, TOOL, "golden", str(out), *gc.case_names()], check=True, timeout=900)
     return out

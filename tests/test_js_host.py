@@ -27,19 +27,8 @@ MAT_DT = np.dtype([("type", "<i4"), ("_pad", "<i4"), ("albedo", "<f8", 3), ("rou
                    ("emission", "<f8", 3)])
 
 
-def ensure_mesh50k():
-    p = os.path.join(SCENES_DIR, "mesh50k.json")
-    if not os.path.exists(p) or os.path.getsize(p) == 0:
-        from blenderraytracer_amd import scene as sc
-        data = sc.load_scene_json("mesh50k")  # generated before the file exists (no empty-file race)
-        tmp = p + f".tmp{os.getpid()}"
-        with open(tmp, "w") as f:
-            json.dump(data, f)
-        os.replace(tmp, p)
-
-
 def run_tool(*args, env=None):
-    ensure_mesh50k()
+    gc.ensure_mesh50k_file()
     out = subprocess.run([NODE, TOOL, *args], cwd=ROOT, capture_output=True, env=env, timeout=600)
     assert out.returncode == 0, out.stderr.decode()[-3000:]
     return out.stdout
