@@ -65,6 +65,10 @@ def parse():
     ap.add_argument("--cpu-crop", type=int, default=64, help="side of the square crop the CPU oracle renders")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 counter passes (N=1 roofline)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse N ranks on fewer GPUs (rank -> device LOCAL_RANK %% device count, sums "
+                         "reduced through host memory); never a measurement")
+    ap.add_argument("--dump", help="rank 0 writes the frame's float64 sums and RGBA8 here (.npz) after the timed steps")
     return ap.parse_args()
 
 
@@ -246,9 +250,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    if args.dist_backend == "gloo":
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     rt = make_tracer(cfg, args.precision, args.seed, local, args.accel)
     packed = rt.packed()
     flops_per_segment = sum(FLOPS[k] * (o.count if k in ("mesh", "triangle") else 1)
@@ -276,10 +285,14 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    if args.dump and rank == 0:
+        import numpy as np
+        torch.cuda.synchronize()
+        np.savez(args.dump, sum=job.sum.cpu().numpy(), rgba8=job.rgba8.cpu().numpy(), samples=job.samples)
 
     e2e = e2e_node = None
     if rank == 0 and world == 1 and not args.no_end_to_end:
@@ -367,7 +380,9 @@ def main():
             "config": {"workload": f"config{cfg['cfg']}_{args.config}_{cfg['w']}x{cfg['h']}_{cfg['spp']}spp",
                        "scene": cfg["scene"], "width": cfg["w"], "height": cfg["h"], "spp": cfg["spp"],
                        "max_depth": cfg["depth"], "primitives": packed.primitives_per_segment(), "accel": args.accel,
-                       "parallelism": f"sample-split x{world} + RCCL reduce" if world > 1 else "1 GPU"},
+                       "parallelism": (f"sample-split x{world} + RCCL reduce" if args.dist_backend == "nccl" else
+                                       f"REHEARSAL sample-split x{world} over {torch.cuda.device_count()} GPU(s), "
+                                       "gloo host reduce: not a measurement") if world > 1 else "1 GPU"},
             "roofline": roofline,
             "roofline_binding": binding,
             "valu_flops": {"achieved": round(flops / (k_ms * 1e-3) / 1e12, 3), "peak": VALU_PEAK_TFLOPS[args.precision],

@@ -23,7 +23,14 @@ def sample_range(rank, world, samples):
 def reduce_sums(buf, world, group=None):
     """Sum the per-pixel radiance sums of all ranks into rank 0's buffer (RCCL reduce on GPUs)."""
     if world > 1:
-        dist.reduce(buf, dst=0, op=dist.ReduceOp.SUM, group=group)
+        if buf.is_cuda and dist.get_backend(group) == "gloo":
+            # gloo reduces host tensors only: the N-ranks-on-fewer-GPUs rehearsal (bench.py
+            # --dist-backend gloo) stages the sums through host memory
+            host = buf.cpu()
+            dist.reduce(host, dst=0, op=dist.ReduceOp.SUM, group=group)
+            buf.copy_(host)
+        else:
+            dist.reduce(buf, dst=0, op=dist.ReduceOp.SUM, group=group)
     return buf
 
 

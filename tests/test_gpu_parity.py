@@ -465,3 +465,33 @@ def test_config4_rtow_4k_1024spp_sharded(gpu):
         assert np.array_equal(o["segments"], g["segments"])
         assert rel_err(b[y0:y0 + 16, x0:x0 + 16] / S, o["mean"]) <= 1e-12
     rt.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_multi_rank_rehearsal(gpu, tmp_path, world):
+    """bench.py's N>1 branch run end to end on the one GPU: `torch.distributed.run` with `world` ranks
+    sharing device 0 (--dist-backend gloo: RCCL refuses two ranks on one device, so the sums are
+    reduced through host memory; everything else — the sample-range split, the barriers, the
+    max-over-ranks time, rank 0's epilogue and JSON line — is the RCCL path's code).  Rank 0's frame
+    equals the 1-rank bench's frame up to the order of the `world` partial-sum additions."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    common = ["--config", "cornell", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-end-to-end", "--no-pmc"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    one = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *common, "--dump", str(tmp_path / "n1.npz")],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert one.returncode == 0, one.stderr[-2000:]
+    multi = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+                            "--master-addr", "127.0.0.1", "--master-port", str(29611 + world),
+                            os.path.join(root, "bench.py"), "--gpus", str(world), "--dist-backend", "gloo", *common,
+                            "--dump", str(tmp_path / "nw.npz")], env=env, capture_output=True, text=True, timeout=300)
+    assert multi.returncode == 0, multi.stderr[-3000:]
+    line = json.loads([ln for ln in multi.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == world and line["value"] > 0 and "REHEARSAL" in line["config"]["parallelism"]
+    a, b = np.load(tmp_path / "n1.npz"), np.load(tmp_path / "nw.npz")
+    assert int(a["samples"]) == int(b["samples"]) == 64
+    assert np.allclose(a["sum"], b["sum"], rtol=SUM_RTOL, atol=1e-300)
+    assert np.mean(a["rgba8"] == b["rgba8"]) > 0.999
