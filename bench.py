@@ -2,6 +2,7 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config rtow|cornell|rtow4k|mesh50k|sample_scene]
                     [--precision f64|f32] [--no-cpu-baseline] [--no-end-to-end] [--no-pmc]
+                    [--dist-backend nccl|gloo] [--dump frame.npz]
 
 A "step" renders one full frame of the workload: every pixel x every sample, traced on the GPU(s)
 from a scene already resident in HBM, the per-pixel float64 sums RCCL-reduced to rank 0 (N>1), and
