@@ -274,14 +274,15 @@ bool trace_uses_pool() {
     return v == 1;
 }
 
-// Samples per pool wave: ~4 sqrt(ns) (0.75 sqrt(ns) when the scene has a triangle BVH: its walks
-// vary more in length, so shorter waves pay), halved (>= 4) until the launch has >= 64k waves (4x the
-// chip's 16k wave slots).  Short waves shorten the frame's drain tail; long ones shorten each wave's
-// own tail (its last items finish at different times) and write fewer chunk partials (each chunk is
-// 24 B per pixel written and read back once).  Measured (LDS-accumulating pool, 1080p): RTOW 512 spp
-// c34 / c48 / c64 / c96 within 0.6 % (c90: 6 chunks, 0.6 GB of partials per frame instead of 1.6);
-// mesh50k 256 spp c12 / c16 / c24 / c32 6786 / 6673 / 6687 / 6391; Cornell 512^2 x 64 spp (4096
-// tiles) 4.  RT_POOL_CHUNK overrides (A/B runs).
+// Samples per pool wave: ~2 sqrt(ns) (0.75 sqrt(ns) when the scene has a triangle BVH: its walks
+// vary more in length, so shorter waves pay), for spheres doubled (up to ~4 sqrt(ns), <= 128) while
+// the launch would have > 400k waves, halved (>= 4) until it has >= 64k waves (4x the chip's 16k wave slots).  Short waves shorten
+// the frame's drain tail; long ones shorten each wave's own tail (its last items finish at different
+// times) and write fewer chunk partials (each chunk is 24 B per pixel written and read back once).
+// Measured (RTOW f64 Msamples/s): 1080p x 512 spp c45 / c90 7477 / 7436; x 256 c32 / c45 /
+// c64 7363 / 7386 / 7295; x 128 c24 / c32 / c45 7330 / 7219 / 7156; x 64 c8 / c16 / c32 6720 / 7015 /
+// 6947; 4K x 128 c23 / c45 7331 / 7393; mesh50k 256 spp c12 / c16 / c24 / c32 6786 / 6673 / 6687 /
+// 6391; Cornell 512^2 x 64 spp (4096 tiles) 4.  RT_POOL_CHUNK overrides (A/B runs).
 static int pool_chunk(int ns, int tiles, bool tri_bvh) {
     static int v = -1;
     if (v == -1) {
@@ -289,7 +290,9 @@ static int pool_chunk(int ns, int tiles, bool tri_bvh) {
         v = e ? std::max(1, atoi(e)) : 0;
     }
     if (v) return v;
-    int c = std::min(128, std::max(4, (int)((tri_bvh ? 0.75 : 4.0) * std::sqrt((double)ns) + 0.5)));
+    int c = std::min(128, std::max(4, (int)((tri_bvh ? 0.75 : 2.0) * std::sqrt((double)ns) + 0.5)));
+    const int cmax = tri_bvh ? c : std::min(128, std::max(4, (int)(4.0 * std::sqrt((double)ns) + 0.5)));
+    while (c < cmax && (long long)tiles * ((ns + c - 1) / c) > 400000) c = std::min(cmax, c * 2);
     while (c > 4 && (long long)tiles * ((ns + c - 1) / c) < 65536) c = std::max(4, c / 2);
     return c;
 }
