@@ -92,7 +92,9 @@ template <class R> struct MatRec { int type, pad; R albedo[3]; R rough; R ior; R
 // contiguous record, so a leaf issues all its loads at once instead of a chain of dependent ones.
 template <class R> struct SphereLeaf { SphereFilter f; SphereRec<R> s; int id, obj, mat, pad; };   // 64 B
 template <> struct SphereLeaf<float> { SphereRec<float> s; int id, obj, mat, pad; };                 // 32 B
-template <class R> struct TriLeaf { TriRec<R> t; int id, obj, mat, pad; };                            // 112 / 64 B
+// a triangle leaf carries only what the test reads (the winner's normal is read from TriRec by hit_record)
+template <class R> struct TriGeom { R v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z; };
+template <class R> struct alignas(16) TriLeaf { TriGeom<R> t; int id, obj, mat, pad; };               // 96 / 64 B
 
 // BVH node (32 B), nodes in depth-first preorder: an internal node's first child is the next node,
 // `skip` is the index just past its subtree.  fc = (first << 4) | count for a leaf of `count` <= 15
@@ -350,8 +352,8 @@ RT_HD bool sphere_candidate(const SphereRec<R>& s, V3<R> o, V3<R> d, R a, R tmin
     return !(t < tmin);
 }
 
-template <class R>
-RT_HD bool triangle_candidate(const TriRec<R>& tr, V3<R> o, V3<R> d, R tmin, R& t) {   // geometry.js:148-188
+template <class R, class Tri>
+RT_HD bool triangle_candidate(const Tri& tr, V3<R> o, V3<R> d, R tmin, R& t) {   // geometry.js:148-188
     R hx = d.y * tr.e2z - d.z * tr.e2y, hy = d.z * tr.e2x - d.x * tr.e2z, hz = d.x * tr.e2y - d.y * tr.e2x;
     R aa = tr.e1x * hx + tr.e1y * hy + tr.e1z * hz;
     if (fabs(aa) < (R)0.0001) return false;
