@@ -21,7 +21,10 @@ ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 
 SOURCES = ["pt_trace.hip", "rt_capi.cpp", "scene_json.cpp"]
+# -structurizecfg-skip-uniform-regions: branches the compiler proves wave-uniform stay plain scalar
+# branches instead of exec-mask regions (RTOW +0.9 %, mesh50k +0.5 %, identical images)
 HIP_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
+             "-mllvm", "-structurizecfg-skip-uniform-regions=1",
              "-Wall", "-Wno-unused-function", "-I", os.path.join(REPO, "include")]
 
 
@@ -38,8 +41,10 @@ def _stale(target, deps):
 
 
 def source_digest():
-    """sha256 (16 hex digits) over the library's sources: csrc/ and include/, names and bytes."""
+    """sha256 (16 hex digits) over the library's sources (csrc/ and include/, names and bytes) and its
+    compile flags (without the machine-specific include path)."""
     h = hashlib.sha256()
+    h.update(" ".join(f for f in HIP_FLAGS if not os.path.isabs(f)).encode())
     for d in (CSRC, os.path.join(REPO, "include")):
         for f in sorted(os.listdir(d)):
             p = os.path.join(d, f)
@@ -61,7 +66,8 @@ def write_build_info():
     """lib/build_info.json: the commit and source digest librt_hip.so was built from (travels with the
     library; bench.py reports it, so a profile names the sources it measured)."""
     info = {"commit": _git("rev-parse", "--short", "HEAD") or None,
-            "sources_modified": bool(_git("status", "--porcelain", "--", CSRC, os.path.join(REPO, "include"))),
+            "sources_modified": bool(_git("status", "--porcelain", "--", CSRC, os.path.join(REPO, "include"),
+                                          os.path.abspath(__file__))),
             "source_digest": source_digest()}
     with open(os.path.join(LIBDIR, "build_info.json"), "w") as f:
         json.dump(info, f)

@@ -11,7 +11,7 @@ for spec in "$@"; do
   objs=""
   for src in $SRCS; do
     obj="$OUT/$name.${src%.*}.o"
-    /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC $flags -I "$ROOT/include" \
+    /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -mllvm -structurizecfg-skip-uniform-regions=1 $flags -I "$ROOT/include" \
       -c "$ROOT/blenderraytracer_amd/csrc/$src" -o "$obj" &
     objs="$objs $obj"
   done
