@@ -2,12 +2,20 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config rtow|cornell|rtow4k|mesh50k|sample_scene]
                     [--precision f64|f32] [--no-cpu-baseline] [--no-end-to-end] [--no-pmc]
-                    [--dist-backend nccl|gloo] [--dump frame.npz]
+                    [--mp-mode ranks|inproc] [--dist-backend nccl|gloo] [--dump frame.npz]
 
 A "step" renders one full frame of the workload: every pixel x every sample, traced on the GPU(s)
 from a scene already resident in HBM, the per-pixel float64 sums RCCL-reduced to rank 0 (N>1), and
 the epilogue (mean, tone map, gamma, RGBA8) run on rank 0's GPU.  Rank r traces samples
 [r*S/N, (r+1)*S/N) of every pixel, so the frame is fixed as N grows ("scaling": "strong").
+
+N > 1, two ways, both runnable as a plain `python bench.py --gpus N`:
+  --mp-mode ranks (default): one process per GPU over torch.distributed (RCCL).  Under
+      torch.distributed.run (WORLD_SIZE set) this process is one rank; without it, this process starts
+      the N rank processes itself (before touching any GPU) and exits with rank 0's status.
+  --mp-mode inproc: one process, rt_settings.devices = [0..N-1] — the split the Node drop-in ships
+      (installGpuRender(rt, {devices})): replicas of the scene, peer copies of the sums over xGMI to
+      device 0, the epilogue there; a step is one rt_render call delivering RGBA8 to the host.
 
 Prints ONE JSON line on rank 0 (driver contract).  The trace step's duration comes from HIP events
 recorded inside librt_hip.so on the stream the kernels run on.  At N=1 (unless --no-pmc) rank 0 then
@@ -66,6 +74,8 @@ def parse():
     ap.add_argument("--cpu-crop", type=int, default=64, help="side of the square crop the CPU oracle renders")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 counter passes (N=1 roofline)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--mp-mode", default="ranks", choices=["ranks", "inproc"],
+                    help="N>1: one process per GPU (torch.distributed) or one process over rt_settings.devices")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks on fewer GPUs (rank -> device LOCAL_RANK %% device count, sums "
                          "reduced through host memory); never a measurement")
@@ -154,6 +164,10 @@ def cpu_baseline(rt, cfg_name, cfg, seed, side):
 # binary64 one for 4: FP64 vector is half the FP32 rate) at 2.4 GHz (MI355X_MICROARCH.md)
 VALU_ISSUE_PEAK_GSLOTS = 256 * 4 * 2.4 / 2
 TRACE_KERNELS = ("trace_pool_kernel", "reduce_kernel")   # the trace step: one launch each per frame
+# the vector-memory data path (TA address / TD data units, vector L1 = TCP, L2 = TCC): TA 1 of 2, TD 1 of 2,
+# TCP 2 of 4, TCC 2 of 4, GRBM 1 of 2 counters per pass
+VMEM_COUNTERS = ("TA_TA_BUSY_sum", "TD_TD_BUSY_sum", "TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum",
+                 "TCC_HIT_sum", "TCC_MISS_sum", "GRBM_GUI_ACTIVE")
 SQ_COUNTERS = ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_INSTS_VALU_ADD_F64",
                "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")
 
@@ -178,7 +192,8 @@ def pmc_passes(args, outdir):
              args.precision, "--seed", str(args.seed), "--accel", args.accel]
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     res = {}
-    for name, counters in (("fetch", ("FETCH_SIZE",)), ("write", ("WRITE_SIZE",)), ("sq", SQ_COUNTERS)):
+    for name, counters in (("fetch", ("FETCH_SIZE",)), ("write", ("WRITE_SIZE",)), ("sq", SQ_COUNTERS),
+                           ("vmem", VMEM_COUNTERS)):
         d = os.path.join(outdir, name)
         cmd = ["timeout", "-s", "KILL", "240", prof, "--pmc", *counters, "--output-format", "csv", "-d", d, "-o", "run",
                "--", *child]
@@ -241,18 +256,53 @@ def build_provenance():
             "library_matches_tree": info.get("source_digest") == tree}
 
 
+def spawn_ranks(args):
+    """`python bench.py --gpus N` without a launcher: start N rank processes (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* in their environment, as torch.distributed.run sets them) and wait for them.
+    This process never touches a GPU (it only starts children); it exits with the first failing rank's
+    status, stopping the other ranks (by their own PIDs) if one fails."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    status = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            rc = p.poll()
+            if rc is None:
+                continue
+            pending.remove(p)
+            if rc != 0 and status == 0:
+                status = rc
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.05)
+    return status
+
+
 def main():
     args = parse()
     if args.pmc_child:
         return pmc_child(args)
     cfg = CONFIGS[args.config]
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and args.mp_mode == "ranks":
+        raise SystemExit(spawn_ranks(args))
+    inproc = args.gpus > 1 and args.mp_mode == "inproc"
+    world = 1 if inproc else int(os.environ.get("WORLD_SIZE", "1"))
+    rank = 0 if inproc else int(os.environ.get("RANK", "0"))
+    local = 0 if inproc else int(os.environ.get("LOCAL_RANK", "0"))
+    if not inproc and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    ndev = torch.cuda.device_count()
     if args.dist_backend == "gloo":
-        local %= torch.cuda.device_count()
+        local %= ndev
     torch.cuda.set_device(local)
     if world > 1:
         if args.dist_backend == "nccl":
@@ -265,10 +315,15 @@ def main():
                             for k, o in zip(packed.kinds, packed.objects))
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and args.gpus == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(rt, args.config, cfg, args.seed, args.cpu_crop)
 
-    job = ShardedRender(rt, rank=rank, world=world, device=torch.device("cuda", local))
+    inproc_devices = [k % ndev for k in range(args.gpus)] if inproc else None
+    if inproc:
+        from blenderraytracer_amd.distributed import InProcessRender
+        job = InProcessRender(rt, inproc_devices)
+    else:
+        job = ShardedRender(rt, rank=rank, world=world, device=torch.device("cuda", local))
     for _ in range(args.warmup):
         job.step()
     torch.cuda.synchronize()
@@ -293,10 +348,14 @@ def main():
     if args.dump and rank == 0:
         import numpy as np
         torch.cuda.synchronize()
-        np.savez(args.dump, sum=job.sum.cpu().numpy(), rgba8=job.rgba8.cpu().numpy(), samples=job.samples)
+        if inproc:      # rt_render's checkpoint holds the frame's merged float64 sums
+            sums, done = rt.checkpoint()
+            np.savez(args.dump, sum=sums.reshape(-1), rgba8=job.rgba8, samples=done)
+        else:
+            np.savez(args.dump, sum=job.sum.cpu().numpy(), rgba8=job.rgba8.cpu().numpy(), samples=job.samples)
 
     e2e = e2e_node = None
-    if rank == 0 and world == 1 and not args.no_end_to_end:
+    if rank == 0 and args.gpus == 1 and not args.no_end_to_end:
         # RayTracer.render as the drop-in boundary runs it (rt_render): sums zeroed on device, the
         # trace, the epilogue, Float32 post-gamma + RGBA8 frames copied back over PCIe
         rt.render()
@@ -325,8 +384,8 @@ def main():
         kernel_desc = "trace step: trace_pool_kernel + reduce_kernel (one launch each per frame)"
         roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                     "traffic": None, "kernel": kernel_desc, "kernel_ms": round(k_ms, 3)}
-        binding = None
-        if world == 1 and not args.no_pmc:
+        binding = vmem = None
+        if args.gpus == 1 and not args.no_pmc:
             import tempfile
             keep = os.environ.get("BENCH_PMC_KEEP")      # scripts/profile_round.sh keeps the counter CSVs
             if keep:
@@ -363,6 +422,23 @@ def main():
                            "waves_per_launch": sq.get("SQ_WAVES"),
                            "source": "rocprofv3 --pmc SQ_* pass over one frame run by this bench invocation / this "
                                      "run's HIP-event trace-step time"}
+                vm = pmc["vmem"]["per_kernel"].get("trace_pool_kernel", {})
+                grbm = vm.get("GRBM_GUI_ACTIVE", 0.0)
+                cu_cycles = 256 * grbm / 8       # rocprofv3's GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles
+                if cu_cycles > 0:
+                    acc = vm.get("TCP_TOTAL_CACHE_ACCESSES_sum", 0.0)
+                    hit, miss = vm.get("TCC_HIT_sum", 0.0), vm.get("TCC_MISS_sum", 0.0)
+                    vmem = {"bound": "vector_memory", "kernel": "trace_pool_kernel",
+                            "td_busy": round(vm.get("TD_TD_BUSY_sum", 0.0) / cu_cycles, 4),
+                            "ta_busy": round(vm.get("TA_TA_BUSY_sum", 0.0) / cu_cycles, 4),
+                            "l1_hit": round(1 - vm.get("TCP_TCC_READ_REQ_sum", 0.0) / acc, 4) if acc else None,
+                            "l2_hit": round(hit / (hit + miss), 4) if hit + miss else None,
+                            "clock_ghz": round(grbm / 8 / (k_ms * 1e-3) / 1e9, 3),
+                            "counters": vm,
+                            "definition": "TA/TD busy cycles summed over the 256 CUs / (256 x GRBM_GUI_ACTIVE / 8): "
+                                          "rocprofv3's GRBM_GUI_ACTIVE is the sum over the 8 XCDs "
+                                          "(MI355X_MICROARCH.md); l1_hit = 1 - TCP_TCC_READ_REQ / TCP accesses",
+                            "source": "rocprofv3 --pmc pass over one frame run by this bench invocation"}
         roofline.update({
             "cache_served_bytes": a_bytes,
             "cache_served_GBps": round(a_bytes / (k_ms * 1e-3) / 1e9, 2),
@@ -373,19 +449,33 @@ def main():
                                         "plane 24, box 24, tri 36) + 12 B/pixel; scalar (SGPR) loads, not HBM"),
             "bvh_nodes_per_segment": round(nodes / seg_launch, 3) if bvh else None,
             "prim_tests_per_segment": round((sph + tri) / seg_launch, 3) if bvh else None})
+        if world > 1:
+            mp_mode = {"mode": "ranks", "world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                       "launcher": "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else "bench.py spawn"}
+            parallelism = (f"sample-split x{world} + RCCL reduce" if args.dist_backend == "nccl" else
+                           f"REHEARSAL sample-split x{world} over {ndev} GPU(s), gloo host reduce: not a measurement")
+        elif inproc:
+            mp_mode = {"mode": "inproc", "devices": inproc_devices}
+            parallelism = (f"in-process sample-split x{args.gpus} (rt_settings.devices {inproc_devices}: peer copies "
+                           "over xGMI + add on device 0)" +
+                           ("" if len(set(inproc_devices)) == args.gpus else
+                            f": REHEARSAL on {ndev} GPU(s), not a measurement"))
+        else:
+            mp_mode = None
+            parallelism = "1 GPU"
         line = {
-            "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
+            "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": args.gpus,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic",
             "config": {"workload": f"config{cfg['cfg']}_{args.config}_{cfg['w']}x{cfg['h']}_{cfg['spp']}spp",
                        "scene": cfg["scene"], "width": cfg["w"], "height": cfg["h"], "spp": cfg["spp"],
                        "max_depth": cfg["depth"], "primitives": packed.primitives_per_segment(), "accel": args.accel,
-                       "parallelism": (f"sample-split x{world} + RCCL reduce" if args.dist_backend == "nccl" else
-                                       f"REHEARSAL sample-split x{world} over {torch.cuda.device_count()} GPU(s), "
-                                       "gloo host reduce: not a measurement") if world > 1 else "1 GPU"},
+                       "parallelism": parallelism},
+            "mp_mode": mp_mode,
             "roofline": roofline,
             "roofline_binding": binding,
+            "roofline_vmem": vmem,
             "valu_flops": {"achieved": round(flops / (k_ms * 1e-3) / 1e12, 3), "peak": VALU_PEAK_TFLOPS[args.precision],
                            "unit": "TFLOP/s", "frac": round(flops / (k_ms * 1e-3) / 1e12 / VALU_PEAK_TFLOPS[args.precision], 4),
                            "flops_per_segment": round(flops / seg_launch, 2),

@@ -9,7 +9,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "librt_hip.so")
 
-RT_ABI_VERSION = 2
+RT_ABI_VERSION = 3
 RT_MAX_DEVICES = 8
 
 # enums (include/rt_hip.h)
@@ -21,6 +21,7 @@ RT_AA_SUPERSAMPLING, RT_AA_STOCHASTIC, RT_AA_CENTER = range(3)
 RT_TM_REINHARD, RT_TM_ACES, RT_TM_LINEAR = range(3)
 RT_PREC_F64, RT_PREC_F32 = range(2)
 RT_ACCEL_AUTO, RT_ACCEL_BRUTE, RT_ACCEL_BVH = range(3)
+RT_SUM_POOL, RT_SUM_SAMPLE_ORDER = range(2)
 
 STATUS = {0: "RT_OK", -1: "RT_ERR_INVALID", -2: "RT_ERR_DEVICE", -3: "RT_ERR_NOMEM",
           -4: "RT_ERR_CANCELLED", -5: "RT_ERR_NO_DEVICE"}
@@ -57,12 +58,13 @@ class Settings(C.Structure):
                 ("crop_x0", C.c_int32), ("crop_y0", C.c_int32), ("crop_w", C.c_int32), ("crop_h", C.c_int32),
                 ("precision", C.c_int32), ("batch_samples", C.c_int32), ("denoise", C.c_int32),
                 ("denoise_weights", C.c_double * 2), ("accel", C.c_int32), ("device_count", C.c_int32),
-                ("devices", C.c_int32 * 8), ("_pad2", C.c_int32)]
+                ("devices", C.c_int32 * 8), ("sum_order", C.c_int32)]
 
 
 class Output(C.Structure):
     _fields_ = [("mean", C.POINTER(C.c_double)), ("post", C.POINTER(C.c_float)), ("rgba8", C.POINTER(C.c_uint8)),
-                ("segments", C.POINTER(C.c_uint32)), ("draws", C.POINTER(C.c_uint32))]
+                ("segments", C.POINTER(C.c_uint32)), ("draws", C.POINTER(C.c_uint32)),
+                ("preview_rgba8", C.POINTER(C.c_uint8))]
 
 
 class Stats(C.Structure):
@@ -88,6 +90,8 @@ EXPORTS = {
     "rt_finalize_device": (C.c_int, [C.c_void_p, C.POINTER(Settings), C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p]),
     "rt_cancel": (C.c_int, [C.c_void_p]),
+    "rt_closest_hits": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_double), C.c_size_t,
+                                  C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "rt_render_checkpoint": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_size_t, C.POINTER(C.c_int32)]),
     "rt_render_resume": (C.c_int, [C.c_void_p, C.POINTER(Settings), C.POINTER(C.c_double), C.c_int32,
                                    C.POINTER(Output), PROGRESS_FN, C.c_void_p, C.POINTER(Stats)]),

@@ -7,13 +7,20 @@
 //                                         (rt_render on a libuv worker thread: the event loop stays live)
 //   cancel(scene)                      -> rt_cancel (polled between sample batches)
 //   destroyScene(scene), deviceCount(), abiVersion()
-// Progress reaches JS through a napi_threadsafe_function; C errors reject the Promise with
-// Error(rt_last_error()).  Built with plain g++ against node_api.h (no node-gyp).
+// Progress reaches JS through a napi_threadsafe_function, in order and before the Promise settles (the
+// worker waits until the main thread has run each call, as the reference calls onProgress inside its
+// loop, ray-tracer.js:256-261); with settings.preview the caller's imageData receives the frame of the
+// samples traced so far at every progress call (the reference's per-row putImageData, :224-241).  The
+// worker thread never writes into JS memory: frames land in job-owned buffers and are copied into the
+// caller's array on the main thread, after checking it was not detached.  C errors reject the Promise
+// with Error(rt_last_error()).  Built with plain g++ against node_api.h (no node-gyp).
 #define NAPI_VERSION 6
 #include <node_api.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <cstdlib>
+#include <mutex>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -69,12 +76,10 @@ int get_int_array(napi_env env, napi_value obj, const char* key, int32_t* out, i
     return len > (uint32_t)max ? -1 : n;
 }
 
-// Raw bytes of a TypedArray / ArrayBuffer / DataView property.
-bool get_bytes(napi_env env, napi_value obj, const char* key, void** data, size_t* bytes) {
-    napi_value v;
+// Raw bytes of a TypedArray / ArrayBuffer / DataView value.
+bool get_bytes_value(napi_env env, napi_value v, void** data, size_t* bytes) {
     *data = nullptr;
     *bytes = 0;
-    if (!get_prop(env, obj, key, &v)) return false;
     bool is;
     if (napi_is_typedarray(env, v, &is) == napi_ok && is) {
         napi_typedarray_type t;
@@ -100,6 +105,15 @@ bool get_bytes(napi_env env, napi_value obj, const char* key, void** data, size_
         return true;
     }
     return false;
+}
+
+// ... of a property
+bool get_bytes(napi_env env, napi_value obj, const char* key, void** data, size_t* bytes) {
+    napi_value v;
+    *data = nullptr;
+    *bytes = 0;
+    if (!get_prop(env, obj, key, &v)) return false;
+    return get_bytes_value(env, v, data, bytes);
 }
 
 // The External owns a SceneBox: destroyScene() frees the device scene eagerly, the GC finalizer
@@ -189,12 +203,18 @@ struct RenderJob {
     bool want_mean = false, want_counts = false, want_post = true;
     // outputs live in JS ArrayBuffers created on the main thread before the work is queued (kept alive
     // by references, not visible to JS until the promise resolves): rt_render copies the frames from
-    // HBM straight into them, with no staging vectors and no copy into the result.  settings.outRgba8
-    // (the caller's imageData.data) receives the RGBA8 frame in place.
+    // HBM straight into them.  settings.outRgba8 (the caller's imageData.data) is written only on the
+    // main thread: the final frame in complete(), preview frames in call_progress.
     enum { OUT_POST, OUT_RGBA, OUT_MEAN, OUT_SEGS, OUT_DRAWS, OUT_N };
     napi_ref out_ref[OUT_N] = {};
     void* out_ptr[OUT_N] = {};
-    bool rgba_is_caller = false;
+    napi_ref caller_rgba = nullptr;  // settings.outRgba8
+    std::vector<uint8_t> preview;    // rt_output.preview_rgba8 (settings.preview)
+    // progress hand-off: the worker waits until the main thread ran the JS callback
+    std::mutex m;
+    std::condition_variable cv;
+    bool pending = false;
+    double fraction = 0;
     rt_stats stats{};
     int status = 0;
     std::string error;
@@ -203,20 +223,47 @@ struct RenderJob {
     int32_t resume_done = -1;
 };
 
+// The caller's typed array behind `ref` if it is still attached and holds `bytes` bytes, else nullptr.
+uint8_t* live_bytes(napi_env env, napi_ref ref, size_t bytes) {
+    napi_value v;
+    if (!ref || napi_get_reference_value(env, ref, &v) != napi_ok || !v) return nullptr;
+    void* p = nullptr;
+    size_t got = 0;
+    if (!get_bytes_value(env, v, &p, &got) || got != bytes) return nullptr;   // detached: length 0
+    return static_cast<uint8_t*>(p);
+}
+
 void call_progress(napi_env env, napi_value js_cb, void*, void* data) {
-    double* frac = static_cast<double*>(data);
-    if (env && js_cb) {
-        napi_value arg, undef;
-        napi_create_double(env, *frac, &arg);
-        napi_get_undefined(env, &undef);
-        napi_call_function(env, undef, js_cb, 1, &arg, nullptr);
+    RenderJob* job = static_cast<RenderJob*>(data);     // alive: the worker waits for this call
+    if (env) {
+        if (!job->preview.empty())
+            if (uint8_t* dst = live_bytes(env, job->caller_rgba, job->preview.size()))
+                std::memcpy(dst, job->preview.data(), job->preview.size());
+        if (js_cb) {
+            napi_value arg, undef;
+            napi_create_double(env, job->fraction, &arg);
+            napi_get_undefined(env, &undef);
+            napi_call_function(env, undef, js_cb, 1, &arg, nullptr);
+        }
     }
-    delete frac;
+    std::lock_guard<std::mutex> lk(job->m);
+    job->pending = false;
+    job->cv.notify_all();
 }
 
 int progress_hook(double fraction, void* user) {
     RenderJob* job = static_cast<RenderJob*>(user);
-    if (job->tsfn) napi_call_threadsafe_function(job->tsfn, new double(fraction), napi_tsfn_nonblocking);
+    if (job->tsfn) {
+        {
+            std::lock_guard<std::mutex> lk(job->m);
+            job->pending = true;
+            job->fraction = fraction;
+        }
+        if (napi_call_threadsafe_function(job->tsfn, job, napi_tsfn_blocking) == napi_ok) {
+            std::unique_lock<std::mutex> lk(job->m);
+            job->cv.wait(lk, [job] { return !job->pending; });
+        }
+    }
     return job->cancel_from_js.load();
 }
 
@@ -228,6 +275,7 @@ void execute(napi_env, void* data) {
     out.mean = static_cast<double*>(job->out_ptr[RenderJob::OUT_MEAN]);
     out.segments = static_cast<uint32_t*>(job->out_ptr[RenderJob::OUT_SEGS]);
     out.draws = static_cast<uint32_t*>(job->out_ptr[RenderJob::OUT_DRAWS]);
+    out.preview_rgba8 = job->preview.empty() ? nullptr : job->preview.data();
     if (job->resume_done >= 0)
         job->status = rt_render_resume(job->scene, &job->st, job->resume.data(), job->resume_done, &out, progress_hook,
                                        job, &job->stats);
@@ -247,7 +295,6 @@ bool make_out(napi_env env, RenderJob* job, int slot, size_t bytes) {
 napi_value out_array(napi_env env, RenderJob* job, int slot, napi_typedarray_type t, size_t len) {
     napi_value v, arr;
     napi_get_reference_value(env, job->out_ref[slot], &v);
-    if (slot == RenderJob::OUT_RGBA && job->rgba_is_caller) return v;
     napi_create_typedarray(env, t, len, v, 0, &arr);
     return arr;
 }
@@ -265,6 +312,18 @@ napi_value to_typed(napi_env env, const std::vector<T>& v, napi_typedarray_type 
 void complete(napi_env env, napi_status, void* data) {
     RenderJob* job = static_cast<RenderJob*>(data);
     if (job->tsfn) napi_release_threadsafe_function(job->tsfn, napi_tsfn_release);
+    // the caller's imageData.data: the finished frame, or after a cancel the frame of the checkpointed
+    // samples (rt_output.preview_rgba8); a buffer detached or transferred meanwhile fails the render
+    if (job->caller_rgba && (job->status == RT_OK || (job->status == RT_ERR_CANCELLED && !job->preview.empty()))) {
+        uint8_t* dst = live_bytes(env, job->caller_rgba, job->n * 4);
+        const uint8_t* src = job->status == RT_OK ? static_cast<const uint8_t*>(job->out_ptr[RenderJob::OUT_RGBA])
+                                                  : job->preview.data();
+        if (dst) std::memcpy(dst, src, job->n * 4);
+        else if (job->status == RT_OK) {
+            job->status = RT_ERR_INVALID;
+            job->error = "render: settings.outRgba8 was detached or resized while rendering";
+        }
+    }
     if (job->status != RT_OK) {
         napi_value msg, err, code;
         napi_create_string_utf8(env, job->error.c_str(), NAPI_AUTO_LENGTH, &msg);
@@ -277,7 +336,10 @@ void complete(napi_env env, napi_status, void* data) {
         napi_create_object(env, &res);
         if (job->want_post)
             napi_set_named_property(env, res, "post", out_array(env, job, RenderJob::OUT_POST, napi_float32_array, job->n * 4));
-        napi_set_named_property(env, res, "rgba8", out_array(env, job, RenderJob::OUT_RGBA, napi_uint8_clamped_array, job->n * 4));
+        napi_value rgba;
+        if (job->caller_rgba) napi_get_reference_value(env, job->caller_rgba, &rgba);
+        else rgba = out_array(env, job, RenderJob::OUT_RGBA, napi_uint8_clamped_array, job->n * 4);
+        napi_set_named_property(env, res, "rgba8", rgba);
         if (job->want_mean) napi_set_named_property(env, res, "mean", out_array(env, job, RenderJob::OUT_MEAN, napi_float64_array, job->n * 3));
         if (job->want_counts) {
             napi_set_named_property(env, res, "segments", out_array(env, job, RenderJob::OUT_SEGS, napi_uint32_array, job->n));
@@ -299,6 +361,7 @@ void complete(napi_env env, napi_status, void* data) {
     job->box->busy = false;
     for (napi_ref r : job->out_ref)
         if (r) napi_delete_reference(env, r);
+    if (job->caller_rgba) napi_delete_reference(env, job->caller_rgba);
     napi_delete_reference(env, job->scene_ref);
     napi_delete_async_work(env, job->work);
     delete job;
@@ -365,19 +428,18 @@ napi_value render(napi_env env, napi_callback_info info) {
         job->resume.assign(static_cast<double*>(rs), static_cast<double*>(rs) + job->n * 3);
         job->resume_done = (int32_t)get_num(env, s, "resumeSamplesDone", 0);
     }
-    // output buffers (see RenderJob): post unless settings.wantPost is 0, RGBA8 into settings.outRgba8
-    // when it is the frame's size
+    st.sum_order = (int32_t)get_num(env, s, "sumOrder", RT_SUM_POOL);
+    // output buffers (see RenderJob): post unless settings.wantPost is 0; the RGBA8 frame also goes into
+    // settings.outRgba8 when that is the frame's size; settings.preview: running frames into it too
     bool ok = !job->want_post || make_out(env, job, RenderJob::OUT_POST, job->n * 4 * sizeof(float));
+    if (ok) ok = make_out(env, job, RenderJob::OUT_RGBA, job->n * 4);
     void* rgba_p = nullptr;
     size_t rgba_bytes = 0;
     napi_value rgba_v;
     if (ok && get_bytes(env, s, "outRgba8", &rgba_p, &rgba_bytes) && rgba_bytes == job->n * 4 &&
         get_prop(env, s, "outRgba8", &rgba_v)) {
-        job->out_ptr[RenderJob::OUT_RGBA] = rgba_p;
-        job->rgba_is_caller = true;
-        ok = napi_create_reference(env, rgba_v, 1, &job->out_ref[RenderJob::OUT_RGBA]) == napi_ok;
-    } else if (ok) {
-        ok = make_out(env, job, RenderJob::OUT_RGBA, job->n * 4);
+        ok = napi_create_reference(env, rgba_v, 1, &job->caller_rgba) == napi_ok;
+        if (ok && get_num(env, s, "preview", 0) != 0) job->preview.assign(job->n * 4, 0);
     }
     if (ok && job->want_mean) ok = make_out(env, job, RenderJob::OUT_MEAN, job->n * 3 * sizeof(double));
     if (ok && job->want_counts) ok = make_out(env, job, RenderJob::OUT_SEGS, job->n * sizeof(uint32_t)) &&
@@ -385,6 +447,7 @@ napi_value render(napi_env env, napi_callback_info info) {
     if (!ok) {
         for (napi_ref r : job->out_ref)
             if (r) napi_delete_reference(env, r);
+        if (job->caller_rgba) napi_delete_reference(env, job->caller_rgba);
         delete job;
         return throw_err(env, "render: cannot allocate the output buffers");
     }

@@ -24,12 +24,31 @@ struct Counters {
     size_t part_bytes = 0;
 };
 
-// bvh: walk the BVHs (ACC_BVH_STACK, the ordered two-child walk), else World order (ACC_BRUTE)
+// bvh: walk the BVHs (ACC_BVH_STACK, the ordered two-child walk), else World order (ACC_BRUTE).
+// pool: the sample-pool kernel (+ reduce_kernel when there are several chunks), else the lane-per-pixel
+// kernel (samples added in sample order, rt_settings.sum_order = RT_SUM_SAMPLE_ORDER)
 template <class R>
-hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh, hipStream_t stream);
+hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh, bool pool,
+                        hipStream_t stream);
 
-// true: launch_trace runs the sample-pool kernel; RT_SAMPLE_POOL=0 in the environment selects the
-// lane-per-pixel kernel (A/B runs, tests)
+// the sample pool's split of `ns` samples of a cw x ch crop: 8x8 tiles, samples per chunk, chunks and the
+// bytes of all chunk partials of one launch
+struct PoolPlan { int tiles, chunk, chunks; size_t part_bytes; };
+PoolPlan pool_plan(int cw, int ch, int ns, bool tri_bvh);
+// the pool kernel writing every chunk (even one) into `part` (>= pool_plan(..).part_bytes), sums untouched:
+// batches may trace concurrently on several streams; launch_reduce then adds part to sum in chunk order
+template <class R>
+hipError_t launch_trace_partials(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh,
+                                 double* part, size_t part_bytes, hipStream_t stream);
+hipError_t launch_reduce(const ImageParams& im, double* sum, const double* part, bool tri_bvh, hipStream_t stream);
+
+// World.hit of n rays (n x 6 doubles, device) -> t, kind, index (device): rt_closest_hits
+template <class R>
+hipError_t launch_closest_hits(const SceneView<R>& sc, bool bvh, const double* rays, size_t n, double* t, int* kind,
+                               int* idx, hipStream_t stream);
+
+// default of rt_settings.sum_order = RT_SUM_POOL: the sample pool, unless RT_SAMPLE_POOL=0 is set in the
+// environment (A/B runs of the lane-per-pixel kernel)
 bool trace_uses_pool();
 // scratch bytes the sample pool needs to trace `ns` samples of a cw x ch crop in one launch (0: one
 // chunk, the partials go straight to the sums).  With less scratch (but at least one chunk's worth,

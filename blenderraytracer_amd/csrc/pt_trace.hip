@@ -313,6 +313,14 @@ size_t pool_partial_bytes(int cw, int ch, int ns, bool tri_bvh) {
 }
 
 template <class R, int ACC>
+static void launch_pool_kernel(const TraceArgs<R>& a, bool count, double* part, int tiles, int chunks, int chunk,
+                               hipStream_t stream) {
+    const size_t lds = stack_lds_bytes<ACC>(a.sc);
+    if (count) hipLaunchKernelGGL((trace_pool_kernel<R, true, ACC>), dim3(tiles * chunks), dim3(64), lds, stream, a, part, tiles, chunk);
+    else hipLaunchKernelGGL((trace_pool_kernel<R, false, ACC>), dim3(tiles * chunks), dim3(64), lds, stream, a, part, tiles, chunk);
+}
+
+template <class R, int ACC>
 static hipError_t launch_pool(const TraceArgs<R>& a0, bool count, hipStream_t stream) {
     const ImageParams& im = a0.im;
     const int ns_all = im.s_end - im.s_begin;
@@ -336,9 +344,7 @@ static hipError_t launch_pool(const TraceArgs<R>& a0, bool count, hipStream_t st
         const int ns = a.im.s_end - b, chunks = (ns + chunk - 1) / chunk;
         if ((long long)tiles * chunks > 0x7FFFFFFFLL) return hipErrorInvalidConfiguration;
         double* part = chunks > 1 ? a0.c.part : nullptr;
-        const size_t lds = stack_lds_bytes<ACC>(a.sc);
-        if (count) hipLaunchKernelGGL((trace_pool_kernel<R, true, ACC>), dim3(tiles * chunks), dim3(64), lds, stream, a, part, tiles, chunk);
-        else hipLaunchKernelGGL((trace_pool_kernel<R, false, ACC>), dim3(tiles * chunks), dim3(64), lds, stream, a, part, tiles, chunk);
+        launch_pool_kernel<R, ACC>(a, count, part, tiles, chunks, chunk, stream);
         if (part)
             hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, stream, a.im, a.c.sum,
                                (const double*)part, tiles, chunks);
@@ -359,8 +365,8 @@ static int bvh_walk_mode() {
 }
 
 template <class R, int ACC>
-static hipError_t launch_acc(const TraceArgs<R>& a, bool count, hipStream_t stream) {
-    if (trace_uses_pool()) return launch_pool<R, ACC>(a, count, stream);
+static hipError_t launch_acc(const TraceArgs<R>& a, bool count, bool pool, hipStream_t stream) {
+    if (pool) return launch_pool<R, ACC>(a, count, stream);
     const int tiles = crop_tiles(a.im.cw, a.im.ch);
     const size_t lds = stack_lds_bytes<ACC>(a.sc);
     if (count) hipLaunchKernelGGL((trace_kernel<R, true, ACC>), dim3(tiles), dim3(64), lds, stream, a);
@@ -369,18 +375,96 @@ static hipError_t launch_acc(const TraceArgs<R>& a, bool count, hipStream_t stre
 }
 
 template <class R>
-hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh,
+hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh, bool pool,
                         hipStream_t stream) {
     if (im.cw <= 0 || im.ch <= 0 || im.s_end <= im.s_begin) return hipSuccess;
     TraceArgs<R> a{sc, im, c};
     const bool count = c.segs || c.draws;
-    if (!bvh) return launch_acc<R, ACC_BRUTE>(a, count, stream);
-    if (bvh_walk_mode() == ACC_BVH) return launch_acc<R, ACC_BVH>(a, count, stream);
-    return launch_acc<R, ACC_BVH_STACK>(a, count, stream);
+    if (!bvh) return launch_acc<R, ACC_BRUTE>(a, count, pool, stream);
+    if (bvh_walk_mode() == ACC_BVH) return launch_acc<R, ACC_BVH>(a, count, pool, stream);
+    return launch_acc<R, ACC_BVH_STACK>(a, count, pool, stream);
 }
 
-template hipError_t launch_trace<double>(const SceneView<double>&, const ImageParams&, const Counters&, bool, hipStream_t);
-template hipError_t launch_trace<float>(const SceneView<float>&, const ImageParams&, const Counters&, bool, hipStream_t);
+template hipError_t launch_trace<double>(const SceneView<double>&, const ImageParams&, const Counters&, bool, bool, hipStream_t);
+template hipError_t launch_trace<float>(const SceneView<float>&, const ImageParams&, const Counters&, bool, bool, hipStream_t);
+
+PoolPlan pool_plan(int cw, int ch, int ns, bool tri_bvh) {
+    PoolPlan p{0, 0, 0, 0};
+    if (cw <= 0 || ch <= 0 || ns <= 0) return p;
+    p.tiles = crop_tiles(cw, ch);
+    p.chunk = pool_chunk(ns, p.tiles, tri_bvh);
+    p.chunks = (ns + p.chunk - 1) / p.chunk;
+    p.part_bytes = (size_t)p.chunks * p.tiles * kPartialBytesPerTile;
+    return p;
+}
+
+// The pool kernel alone, every chunk (even a single one) into `part`: the sums are not touched, so
+// several such launches (batches) may run at once on different streams; launch_reduce adds them.
+template <class R, int ACC>
+static hipError_t launch_partials_acc(const TraceArgs<R>& a, bool count, const PoolPlan& p, double* part,
+                                      hipStream_t stream) {
+    if ((long long)p.tiles * p.chunks > 0x7FFFFFFFLL) return hipErrorInvalidConfiguration;
+    launch_pool_kernel<R, ACC>(a, count, part, p.tiles, p.chunks, p.chunk, stream);
+    return hipGetLastError();
+}
+
+template <class R>
+hipError_t launch_trace_partials(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh,
+                                 double* part, size_t part_bytes, hipStream_t stream) {
+    if (im.cw <= 0 || im.ch <= 0 || im.s_end <= im.s_begin) return hipSuccess;
+    const PoolPlan p = pool_plan(im.cw, im.ch, im.s_end - im.s_begin, sc.num_tri_nodes > 0);
+    if (!part || part_bytes < p.part_bytes) return hipErrorInvalidValue;
+    TraceArgs<R> a{sc, im, c};
+    const bool count = c.segs || c.draws;
+    if (!bvh) return launch_partials_acc<R, ACC_BRUTE>(a, count, p, part, stream);
+    if (bvh_walk_mode() == ACC_BVH) return launch_partials_acc<R, ACC_BVH>(a, count, p, part, stream);
+    return launch_partials_acc<R, ACC_BVH_STACK>(a, count, p, part, stream);
+}
+
+template hipError_t launch_trace_partials<double>(const SceneView<double>&, const ImageParams&, const Counters&, bool,
+                                                  double*, size_t, hipStream_t);
+template hipError_t launch_trace_partials<float>(const SceneView<float>&, const ImageParams&, const Counters&, bool,
+                                                 double*, size_t, hipStream_t);
+
+hipError_t launch_reduce(const ImageParams& im, double* sum, const double* part, bool tri_bvh, hipStream_t stream) {
+    if (im.cw <= 0 || im.ch <= 0 || im.s_end <= im.s_begin) return hipSuccess;
+    const PoolPlan p = pool_plan(im.cw, im.ch, im.s_end - im.s_begin, tri_bvh);
+    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((p.tiles + 3) / 4)), dim3(256), 0, stream, im, sum, part, p.tiles,
+                       p.chunks);
+    return hipGetLastError();
+}
+
+// ---- World.hit for given rays (rt_closest_hits: the BVH proof on device arithmetic) ----
+template <class R, int ACC>
+__global__ __launch_bounds__(64) void closest_hits_kernel(const SceneView<R> sc, const double* __restrict__ rays,
+                                                          const size_t n, double* __restrict__ t_out,
+                                                          int* __restrict__ kind_out, int* __restrict__ idx_out) {
+    __shared__ int stack[RT_BVH_STACK * 64];
+    const BvhStack stk{stack + threadIdx.x, 64};
+    const size_t r = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (r >= n) return;
+    const double* q = rays + 6 * r;
+    const V3<R> o = mk<R>((R)q[0], (R)q[1], (R)q[2]), d = mk<R>((R)q[3], (R)q[4], (R)q[5]);
+    Work w{0, 0, 0, 0, 0, 0};
+    const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, w, stk);
+    t_out[r] = c.kind == HIT_NONE ? (double)INFINITY : (double)c.t;
+    kind_out[r] = c.kind;
+    idx_out[r] = c.kind == HIT_NONE ? -1 : c.idx;
+}
+
+template <class R>
+hipError_t launch_closest_hits(const SceneView<R>& sc, bool bvh, const double* rays, size_t n, double* t, int* kind,
+                               int* idx, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 63) / 64));
+    if (bvh) hipLaunchKernelGGL((closest_hits_kernel<R, ACC_BVH_STACK>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);
+    else hipLaunchKernelGGL((closest_hits_kernel<R, ACC_BRUTE>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);
+    return hipGetLastError();
+}
+template hipError_t launch_closest_hits<double>(const SceneView<double>&, bool, const double*, size_t, double*, int*, int*,
+                                                hipStream_t);
+template hipError_t launch_closest_hits<float>(const SceneView<float>&, bool, const double*, size_t, double*, int*, int*,
+                                               hipStream_t);
 
 // ---- multi-device sample split: dst += src elementwise (the shards' sums / counters, in shard order) ----
 template <class T>

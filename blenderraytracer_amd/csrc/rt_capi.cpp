@@ -147,16 +147,21 @@ struct DeviceState {
     int device = 0;
     DeviceScene<double> s64;
     DeviceScene<float> s32;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // accumulation stream: zeroing, reduces, merges, epilogue
     hipEvent_t ev[2] = {};             // trace timing
     DevBuf<double> sum;
     DevBuf<uint32_t> segs, draws;
     DevBuf<unsigned long long> total;
-    DevBuf<double> part;               // sample-pool chunk partials (ensure_partials)
+    DevBuf<double> part;               // sample-pool chunk partials (ensure_partials; overlapped batches: slot 0)
     hipEvent_t scratch_ev = nullptr;   // recorded after every use of part / total (order_scratch)
     hipStream_t scratch_stream = nullptr;
     bool scratch_used = false;
     hipEvent_t copy_ev = nullptr;      // a replica's batch sums copied out to the home device (merge_shards)
+    // overlapped batches (render_impl): batch k traces on tstream[k % 2] into its own partials, so the
+    // next batch's waves fill the CUs while this one drains; its reduce runs on `stream` in batch order
+    hipStream_t tstream[2] = {};
+    DevBuf<double> part2;              // partials of slot 1
+    hipEvent_t traced[2] = {}, reduced[2] = {}, setup_ev = nullptr;
 
     int init(int dev, const HostScene& hs, const rt_scene_desc& d) {
         device = dev;
@@ -165,23 +170,30 @@ struct DeviceState {
         int rc;
         if ((rc = build_device(s64, hs, d)) || (rc = build_device(s32, hs, d))) return rc;
         e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+        for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipStreamCreateWithFlags(&tstream[k], hipStreamNonBlocking);
         for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreate(&ev[k]);
+        for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&traced[k], hipEventDisableTiming);
+        for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&reduced[k], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&setup_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&scratch_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&copy_ev, hipEventDisableTiming);
         if (e != hipSuccess) return fail(RT_ERR_DEVICE, "stream/event create: %s", hipGetErrorString(e));
         return RT_OK;
     }
-    void release() {
+    void sync_all() {                  // every stream of this device (error paths, release)
         (void)hipSetDevice(device);
-        if (stream) (void)hipStreamSynchronize(stream);
+        for (hipStream_t s : {tstream[0], tstream[1], stream})
+            if (s) (void)hipStreamSynchronize(s);
+    }
+    void release() {
+        sync_all();
         s64.release();
         s32.release();
-        sum.release(); segs.release(); draws.release(); total.release(); part.release();
-        for (auto& e : ev)
+        sum.release(); segs.release(); draws.release(); total.release(); part.release(); part2.release();
+        for (hipEvent_t e : {ev[0], ev[1], traced[0], traced[1], reduced[0], reduced[1], setup_ev, scratch_ev, copy_ev})
             if (e) (void)hipEventDestroy(e);
-        if (scratch_ev) (void)hipEventDestroy(scratch_ev);
-        if (copy_ev) (void)hipEventDestroy(copy_ev);
-        if (stream) (void)hipStreamDestroy(stream);
+        for (hipStream_t s : {tstream[0], tstream[1], stream})
+            if (s) (void)hipStreamDestroy(s);
     }
 };
 
@@ -227,6 +239,10 @@ struct rt_scene {
     std::vector<MergeSlot> merge;   // per shard (index in the render's device list): its staging on home
     DevBuf<float> post, post_raw;   // post_raw: pre-denoise floatData
     DevBuf<uint8_t> rgba;
+    DevBuf<uint8_t> preview;        // rt_output.preview_rgba8: the running frame of the last batch (device) ...
+    uint8_t* preview_host[2] = {};  // ... copied into pinned staging (one per in-flight batch)
+    size_t preview_host_n = 0;
+    hipEvent_t batch_done[2] = {};  // home stream: batch k's reduce, merges and preview done (slot k % 2)
     std::atomic<int> cancel{0};
     size_t ckpt_pixels = 0;         // progressive state of the last rt_render / rt_render_resume:
     int ckpt_done = 0;              // `home.sum` holds samples [sample_begin, ckpt_done) of ckpt_pixels pixels
@@ -300,31 +316,86 @@ int check_accel(const rt_scene* sc, const rt_settings* s) {
     return RT_OK;
 }
 
+// rt_settings.sum_order: the sample pool unless the caller asks for sample order (or RT_SAMPLE_POOL=0)
+bool use_pool(const rt_settings* s) { return s->sum_order == RT_SUM_POOL && trace_uses_pool(); }
+
 hipError_t trace(const rt_scene* sc, const DeviceState& ds, const rt_settings* s, const ImageParams& im,
                  const Counters& c, hipStream_t st) {
     if (im.max_depth <= 0) return hipSuccess;   // rayColor(ray, depth<=0) is 0: nothing to trace
+    const bool bvh = use_bvh(sc, s), pool = use_pool(s);
+    if (s->precision == RT_PREC_F32) return launch_trace<float>(ds.s32.view, im, c, bvh, pool, st);
+    return launch_trace<double>(ds.s64.view, im, c, bvh, pool, st);
+}
+
+// One overlapped batch on one device: the pool kernel writes the batch's chunk partials into slot `j`
+// on tstream[j] (after the reduce that last read slot j), and `stream` adds them to the sums in chunk
+// order once the trace is done.  Sums see the same additions in the same order as trace() of the batch
+// (bit-identical), while the trace of batch k+1 may already run beside batch k's draining waves.
+hipError_t trace_overlapped(const rt_scene* sc, DeviceState& ds, const rt_settings* s, const ImageParams& im,
+                            const Counters& c, int j, bool slot_used) {
+    if (im.max_depth <= 0 || im.s_end <= im.s_begin) return hipSuccess;
     const bool bvh = use_bvh(sc, s);
-    if (s->precision == RT_PREC_F32) return launch_trace<float>(ds.s32.view, im, c, bvh, st);
-    return launch_trace<double>(ds.s64.view, im, c, bvh, st);
+    DevBuf<double>& part = j == 0 ? ds.part : ds.part2;
+    hipStream_t ts = ds.tstream[j];
+    hipError_t e = hipSuccess;
+    if (slot_used) e = hipStreamWaitEvent(ts, ds.reduced[j], 0);
+    if (e == hipSuccess)
+        e = s->precision == RT_PREC_F32
+                ? launch_trace_partials<float>(ds.s32.view, im, c, bvh, part.p, part.n * sizeof(double), ts)
+                : launch_trace_partials<double>(ds.s64.view, im, c, bvh, part.p, part.n * sizeof(double), ts);
+    if (e == hipSuccess) e = hipEventRecord(ds.traced[j], ts);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ds.stream, ds.traced[j], 0);
+    if (e == hipSuccess) e = launch_reduce(im, c.sum, part.p, sc->tri_bvh, ds.stream);
+    if (e == hipSuccess) e = hipEventRecord(ds.reduced[j], ds.stream);
+    return e;
+}
+
+// Peer access between the scene's device and a replica's (hipMemcpyPeerAsync then runs over xGMI
+// directly instead of a staged copy).  Fails loudly if the two devices have no peer path.
+int enable_peer(int a, int b) {
+    if (a == b) return RT_OK;
+    for (int k = 0; k < 2; ++k) {
+        const int from = k ? b : a, to = k ? a : b;
+        int can = 0;
+        HIP_TRY(hipDeviceCanAccessPeer(&can, from, to));
+        if (!can) return fail(RT_ERR_DEVICE, "device %d cannot access device %d (no peer path for the sample split)", from, to);
+        HIP_TRY(hipSetDevice(from));
+        const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+        if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+        else if (e != hipSuccess) return fail(RT_ERR_DEVICE, "hipDeviceEnablePeerAccess(%d -> %d): %s", from, to, hipGetErrorString(e));
+    }
+    return RT_OK;
 }
 
 // Sample-pool chunk partials (pool_partial_bytes, pt_trace.hip): all of a launch's chunks when they fit
 // the budget (RT_PART_MB, default 2 GiB, at most 10 % of the free device memory), else as many
 // chunks as fit (launch_trace then splits the samples over several launches).  RTOW 1080p x 512 spp
 // needs 0.3 GB; a launch with a single chunk needs none.  Kept by the device state between renders.
-int ensure_partials(const rt_scene* sc, DeviceState& ds, int cw, int ch, int samples, Counters& c) {
-    if (!trace_uses_pool() || samples <= 0 || cw <= 0 || ch <= 0) return RT_OK;
-    const size_t want_all = pool_partial_bytes(cw, ch, samples, sc->tri_bvh);
-    if (want_all == 0) return RT_OK;
-    const size_t per_chunk = (size_t)((cw + 7) / 8) * ((ch + 7) / 8) * kPartialBytesPerTile;
+size_t part_budget() {
     static size_t budget = 0;
     if (!budget) {
         const char* e = getenv("RT_PART_MB");
         budget = (size_t)(e ? std::max(1LL, atoll(e)) : 2048LL) << 20;
     }
+    return budget;
+}
+
+// A device state's scratch may still be read by an asynchronous call on another stream (rt_trace_device):
+// wait for its last user before freeing or reallocating it (hipFree's implicit device synchronization is
+// not relied upon).
+hipError_t scratch_idle(DeviceState& ds) {
+    return ds.scratch_used ? hipEventSynchronize(ds.scratch_ev) : hipSuccess;
+}
+
+int ensure_partials(const rt_scene* sc, DeviceState& ds, int cw, int ch, int samples, bool pool, Counters& c) {
+    if (!pool || samples <= 0 || cw <= 0 || ch <= 0) return RT_OK;
+    const size_t want_all = pool_partial_bytes(cw, ch, samples, sc->tri_bvh);
+    if (want_all == 0) return RT_OK;
+    const size_t per_chunk = (size_t)((cw + 7) / 8) * ((ch + 7) / 8) * kPartialBytesPerTile;
     size_t want = want_all;
     if (want > ds.part.n * sizeof(double)) {
-        size_t free_b = 0, total_b = 0, cap = budget;
+        HIP_TRY(scratch_idle(ds));
+        size_t free_b = 0, total_b = 0, cap = part_budget();
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = std::min(cap, (free_b + ds.part.n * sizeof(double)) / 10);
         want = std::min(want, std::max<size_t>(cap / per_chunk, 1) * per_chunk);
         while (want > ds.part.n * sizeof(double)) {
@@ -337,6 +408,23 @@ int ensure_partials(const rt_scene* sc, DeviceState& ds, int cw, int ch, int sam
     c.part = ds.part.p;
     c.part_bytes = ds.part.n * sizeof(double);
     return RT_OK;
+}
+
+// Both partial slots of the overlapped batches, `bytes` each (one batch's chunks: pool_plan).  False
+// (no error) when they do not fit the budget: the render then runs its batches one after the other.
+bool ensure_overlap_partials(DeviceState& ds, size_t bytes) {
+    const size_t have = std::min(ds.part.n, ds.part2.n) * sizeof(double);
+    if (bytes == 0 || (ds.part.p && ds.part2.p && have >= bytes)) return true;
+    if (scratch_idle(ds) != hipSuccess) return false;
+    size_t free_b = 0, total_b = 0, cap = part_budget();
+    const size_t held = (ds.part.n + ds.part2.n) * sizeof(double);
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = std::min(cap, (free_b + held) / 10);
+    if (2 * bytes > cap) return false;
+    if (ds.part.ensure(bytes / sizeof(double)) != hipSuccess || ds.part2.ensure(bytes / sizeof(double)) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return true;
 }
 
 // A device state's scratch buffers (chunk partials, work totals) are shared by every call on it.  A
@@ -397,8 +485,10 @@ int shard_states(rt_scene* sc, const rt_settings* s, std::vector<DeviceState*>& 
             r = nullptr;
         }
         if (!r) {
+            int rc = enable_peer(sc->home.device, dev);
+            if (rc) return rc;
             r = new DeviceState();
-            const int rc = r->init(dev, sc->hs, sc->desc.d);
+            rc = r->init(dev, sc->hs, sc->desc.d);
             if (rc) {
                 r->release();
                 delete r;
@@ -487,7 +577,10 @@ void rt_scene_destroy(rt_scene* sc) {
         if (m.added) (void)hipEventDestroy(m.added);
     }
     sc->rgba.release();
-    for (auto& e : sc->ev)
+    sc->preview.release();
+    for (uint8_t* p : sc->preview_host)
+        if (p) (void)hipHostFree(p);
+    for (hipEvent_t e : {sc->ev[0], sc->ev[1], sc->batch_done[0], sc->batch_done[1]})
         if (e) (void)hipEventDestroy(e);
     delete sc;
 }
@@ -549,7 +642,15 @@ int merge_shards(rt_scene* sc, const std::vector<DeviceState*>& states, size_t n
     return RT_OK;
 }
 
-// rt_render and rt_render_resume: trace samples [first, sample_end) on top of `sums_in` (NULL: zeros)
+// rt_render and rt_render_resume: trace samples [first, sample_end) on top of `sums_in` (NULL: zeros).
+//
+// Batches (rt_settings.batch_samples) are pipelined: batch k+1 is enqueued before the host waits for
+// batch k, so the GPU never idles on the host's progress call.  With the sample pool and more than one
+// batch, consecutive batches also trace on two streams into their own chunk partials (trace_overlapped):
+// the next batch's waves fill the CUs while the previous one drains, and the reduces add the partials in
+// batch order, so the sums are bit-identical to running the batches one after the other (and to a
+// checkpoint + resume at any batch boundary).  A cancel (progress() returning non-zero, rt_cancel) is
+// observed after a batch: the batch already in flight completes and is part of the checkpoint.
 int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progress_fn progress, void* user,
                 rt_stats* stats, const double* sums_in, int first) {
     const double t_start = now_ms();
@@ -563,25 +664,41 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     sc->cancel.store(0);
     const size_t n = (size_t)cw * ch;
     const bool want_segs = out && out->segments, want_draws = out && out->draws;
+    const bool pool = use_pool(s);
     ImageParams im = image_params(s, cw, ch);
+    const int base = im.s_begin;                  // the sums hold samples [base, done) of every pixel
     im.s_begin = std::max(im.s_begin, first);
     const int s0 = im.s_begin, s1 = std::max(im.s_end, s0);
     const int batch = s->batch_samples > 0 ? s->batch_samples : std::max(1, s1 - s0);
+    const int nb = s1 > s0 ? (s1 - s0 + batch - 1) / batch : 0;
     const int nsh = (int)states.size();
+    DeviceState& h = sc->home;
+    const bool want_preview = out && out->preview_rgba8 && nb > 1;
     std::vector<Counters> cs(nsh);
+    bool overlap = pool && nb > 1 && s->max_depth > 0;
     for (int k = 0; k < nsh; ++k) {
         DeviceState& ds = *states[k];
         HIP_TRY(hipSetDevice(ds.device));
         HIP_TRY(ds.sum.ensure(3 * n));
         HIP_TRY(ds.total.ensure(kTotalSlots));
+        int b0, b1;
+        shard_range(s0, s0 + std::min(batch, s1 - s0), k, nsh, b0, b1);
+        if (overlap) overlap = ensure_overlap_partials(ds, pool_plan(cw, ch, std::max(1, b1 - b0), sc->tri_bvh).part_bytes);
+    }
+    for (int k = 0; k < nsh; ++k) {
+        DeviceState& ds = *states[k];
+        HIP_TRY(hipSetDevice(ds.device));
+        Counters& c = cs[k];
+        c = Counters{ds.sum.p, nullptr, nullptr, ds.total.p};
+        int b0, b1;
+        shard_range(s0, s0 + std::min(batch, s1 - s0), k, nsh, b0, b1);
+        if (!overlap && s->max_depth > 0 && (rc = ensure_partials(sc, ds, cw, ch, std::max(1, b1 - b0), pool, c))) return rc;
         HIP_TRY(order_scratch(ds, ds.stream));
-        if (sums_in && &ds == &sc->home)
+        if (sums_in && &ds == &h)
             HIP_TRY(hipMemcpyAsync(ds.sum.p, sums_in, 3 * n * sizeof(double), hipMemcpyHostToDevice, ds.stream));
         else
             HIP_TRY(hipMemsetAsync(ds.sum.p, 0, 3 * n * sizeof(double), ds.stream));
         HIP_TRY(hipMemsetAsync(ds.total.p, 0, kTotalSlots * sizeof(unsigned long long), ds.stream));
-        Counters& c = cs[k];
-        c = Counters{ds.sum.p, nullptr, nullptr, ds.total.p};
         if (want_segs) {
             HIP_TRY(ds.segs.ensure(n));
             HIP_TRY(hipMemsetAsync(ds.segs.p, 0, n * sizeof(uint32_t), ds.stream));
@@ -592,12 +709,13 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
             HIP_TRY(hipMemsetAsync(ds.draws.p, 0, n * sizeof(uint32_t), ds.stream));
             c.draws = ds.draws.p;
         }
-        int b0, b1;
-        shard_range(s0, s0 + std::min(batch, s1 - s0), k, nsh, b0, b1);
-        if (s->max_depth > 0 && (rc = ensure_partials(sc, ds, cw, ch, std::max(1, b1 - b0), c))) return rc;
+        HIP_TRY(hipEventRecord(ds.ev[0], ds.stream));
+        if (overlap) {                            // the trace streams start after this set-up
+            HIP_TRY(hipEventRecord(ds.setup_ev, ds.stream));
+            for (hipStream_t t : ds.tstream) HIP_TRY(hipStreamWaitEvent(t, ds.setup_ev, 0));
+        }
     }
-    if (states[0] != &sc->home) {                 // the home device only merges: its buffers start here
-        DeviceState& h = sc->home;
+    if (states[0] != &h) {                        // the home device only merges: its buffers start here
         HIP_TRY(hipSetDevice(h.device));
         HIP_TRY(h.sum.ensure(3 * n));
         if (sums_in) HIP_TRY(hipMemcpyAsync(h.sum.p, sums_in, 3 * n * sizeof(double), hipMemcpyHostToDevice, h.stream));
@@ -611,51 +729,101 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
             HIP_TRY(hipMemsetAsync(h.draws.p, 0, n * sizeof(uint32_t), h.stream));
         }
     }
+    HIP_TRY(hipSetDevice(h.device));
+    for (hipEvent_t& e : sc->batch_done)
+        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (want_preview) {
+        HIP_TRY(sc->preview.ensure(4 * n));
+        if (sc->preview_host_n < 4 * n) {
+            for (uint8_t*& p : sc->preview_host) {
+                if (p) (void)hipHostFree(p);
+                p = nullptr;
+            }
+            sc->preview_host_n = 0;
+            for (uint8_t*& p : sc->preview_host) HIP_TRY(hipHostMalloc((void**)&p, 4 * n, hipHostMallocDefault));
+            sc->preview_host_n = 4 * n;
+        }
+    }
     sc->ckpt_pixels = n;
     sc->ckpt_done = s0;
-    double kernel_ms = 0;
-    int status = RT_OK;
-    for (int b = s0; b < s1; b += batch) {
-        const int be = std::min(s1, b + batch);
+
+    // enqueue batch kb (no host wait): every shard's trace, the merge of the shards into the home device,
+    // the preview frame, then batch_done[kb % 2] on the home stream
+    auto enqueue = [&](int kb) -> int {
+        const int b = s0 + kb * batch, be = std::min(s1, b + batch);
         for (int k = 0; k < nsh; ++k) {           // every shard's launches first: the devices run together
             DeviceState& ds = *states[k];
             ImageParams bi = im;
             shard_range(b, be, k, nsh, bi.s_begin, bi.s_end);
             HIP_TRY(hipSetDevice(ds.device));
-            HIP_TRY(hipEventRecord(ds.ev[0], ds.stream));
-            HIP_TRY(trace(sc, ds, s, bi, cs[k], ds.stream));
-            HIP_TRY(hipEventRecord(ds.ev[1], ds.stream));
+            if (overlap) HIP_TRY(trace_overlapped(sc, ds, s, bi, cs[k], kb % 2, kb >= 2));
+            else HIP_TRY(trace(sc, ds, s, bi, cs[k], ds.stream));
         }
-        float batch_ms = 0;
-        for (int k = 0; k < nsh; ++k) {
-            DeviceState& ds = *states[k];
-            HIP_TRY(hipSetDevice(ds.device));
-            HIP_TRY(hipEventSynchronize(ds.ev[1]));
-            float ms = 0;
-            HIP_TRY(hipEventElapsedTime(&ms, ds.ev[0], ds.ev[1]));
-            batch_ms = std::max(batch_ms, ms);
+        int r;
+        if (nsh > 1 && (r = merge_shards(sc, states, n, want_segs, want_draws))) return r;
+        HIP_TRY(hipSetDevice(h.device));
+        if (want_preview) {                       // the running frame: mean over the samples so far
+            FinalizeParams fp{(int)n, be - base, s->tone_map, s->exposure, s->gamma};
+            HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview.p, h.stream));
+            HIP_TRY(hipMemcpyAsync(sc->preview_host[kb % 2], sc->preview.p, 4 * n, hipMemcpyDeviceToHost, h.stream));
         }
-        kernel_ms += batch_ms;
-        if (nsh > 1 && (rc = merge_shards(sc, states, n, want_segs, want_draws))) return rc;
+        HIP_TRY(hipEventRecord(sc->batch_done[kb % 2], h.stream));
+        return RT_OK;
+    };
+    // host side of batch kb once batch_done: checkpoint state and the preview frame
+    auto complete = [&](int kb) -> int {
+        HIP_TRY(hipEventSynchronize(sc->batch_done[kb % 2]));
+        const int be = std::min(s1, s0 + (kb + 1) * batch);
         sc->ckpt_done = be;
-        if (progress && be < s1) {
-            if (progress((double)(be - s0) / (double)(s1 - s0), user)) sc->cancel.store(1);
+        if (want_preview) memcpy(out->preview_rgba8, sc->preview_host[kb % 2], 4 * n);
+        return RT_OK;
+    };
+    int status = RT_OK, enqueued = 0;
+    if (nb > 0) {
+        status = enqueue(0);
+        enqueued = status == RT_OK ? 1 : 0;
+    }
+    for (int kb = 0; kb < nb && status == RT_OK; ++kb) {
+        if (enqueued == kb + 1 && kb + 1 < nb && !sc->cancel.load()) {
+            if ((status = enqueue(kb + 1))) break;
+            enqueued = kb + 2;
         }
+        if ((status = complete(kb))) break;
+        const int be = sc->ckpt_done;
+        if (progress && be < s1 && progress((double)(be - s0) / (double)(s1 - s0), user)) sc->cancel.store(1);
         if (sc->cancel.load()) {
-            status = fail(RT_ERR_CANCELLED, "render cancelled after %d samples", be);
+            if (enqueued > kb + 1 && (status = complete(kb + 1))) break;   // the batch in flight finishes
+            status = fail(RT_ERR_CANCELLED, "render cancelled after %d samples", sc->ckpt_done);
             break;
         }
     }
+    if (status != RT_OK && status != RT_ERR_CANCELLED) {
+        // a HIP error inside the pipeline: drain every stream; the checkpoint keeps the last batch whose
+        // merge is known to be complete (complete() ran for it), and the scratch is released
+        const std::string err = g_error;
+        for (DeviceState* ds : states) {
+            ds->sync_all();
+            (void)release_scratch(*ds, ds->stream);
+        }
+        h.sync_all();
+        (void)hipGetLastError();
+        g_error = err;
+        return status;
+    }
     unsigned long long totals[kTotalSlots] = {};
+    float kernel_ms = 0;
     for (DeviceState* ds : states) {
         unsigned long long t[kTotalSlots] = {};
         HIP_TRY(hipSetDevice(ds->device));
+        HIP_TRY(hipEventRecord(ds->ev[1], ds->stream));
         HIP_TRY(hipMemcpyAsync(t, ds->total.p, sizeof t, hipMemcpyDeviceToHost, ds->stream));
         HIP_TRY(release_scratch(*ds, ds->stream));
         HIP_TRY(hipStreamSynchronize(ds->stream));
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, ds->ev[0], ds->ev[1]));
+        kernel_ms = std::max(kernel_ms, ms);
         for (int k = 0; k < kTotalSlots; ++k) totals[k] += t[k];
     }
-    DeviceState& h = sc->home;
     HIP_TRY(hipSetDevice(h.device));
     HIP_TRY(hipStreamSynchronize(h.stream));          // the merges of the last batch (checkpoint state)
     if (status != RT_OK) return status;
@@ -741,7 +909,7 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
     HIP_TRY(ds.total.ensure(kTotalSlots));
     ImageParams im = image_params(s, cw, ch);
     Counters c{d_sum, nullptr, nullptr, ds.total.p};
-    if (s->max_depth > 0 && (rc = ensure_partials(sc, ds, cw, ch, im.s_end - im.s_begin, c))) return rc;
+    if (s->max_depth > 0 && (rc = ensure_partials(sc, ds, cw, ch, im.s_end - im.s_begin, use_pool(s), c))) return rc;
     HIP_TRY(order_scratch(ds, st));
     HIP_TRY(hipMemsetAsync(ds.total.p, 0, kTotalSlots * sizeof(unsigned long long), st));
     HIP_TRY(hipEventRecord(ds.ev[0], st));
@@ -761,6 +929,40 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
             stats->wall_ms = now_ms() - t_start;
         }
     }
+    return RT_OK;
+}
+
+int rt_closest_hits(rt_scene* sc, int32_t precision, int32_t accel, const double* rays, size_t n, double* t,
+                    int32_t* kind, int32_t* index) {
+    if (!sc || (n > 0 && !rays)) return fail(RT_ERR_INVALID, "NULL argument");
+    if (precision != RT_PREC_F64 && precision != RT_PREC_F32) return fail(RT_ERR_INVALID, "precision %d", precision);
+    rt_settings s{};
+    s.accel = accel;
+    if (s.accel < RT_ACCEL_AUTO || s.accel > RT_ACCEL_BVH) return fail(RT_ERR_INVALID, "accel %d", accel);
+    int rc = check_accel(sc, &s);
+    if (rc) return rc;
+    if (n == 0) return RT_OK;
+    DeviceState& ds = sc->home;
+    HIP_TRY(hipSetDevice(ds.device));
+    DevBuf<double> d_rays, d_t;
+    DevBuf<int> d_kind, d_idx;
+    auto cleanup = [&] { d_rays.release(); d_t.release(); d_kind.release(); d_idx.release(); };
+    hipError_t e = d_rays.ensure(6 * n);
+    if (e == hipSuccess) e = d_t.ensure(n);
+    if (e == hipSuccess) e = d_kind.ensure(n);
+    if (e == hipSuccess) e = d_idx.ensure(n);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_rays.p, rays, 6 * n * sizeof(double), hipMemcpyHostToDevice, ds.stream);
+    const bool bvh = use_bvh(sc, &s);
+    if (e == hipSuccess)
+        e = precision == RT_PREC_F32 ? launch_closest_hits<float>(ds.s32.view, bvh, d_rays.p, n, d_t.p, d_kind.p, d_idx.p, ds.stream)
+                                     : launch_closest_hits<double>(ds.s64.view, bvh, d_rays.p, n, d_t.p, d_kind.p, d_idx.p, ds.stream);
+    if (e == hipSuccess && t) e = hipMemcpyAsync(t, d_t.p, n * sizeof(double), hipMemcpyDeviceToHost, ds.stream);
+    if (e == hipSuccess && kind) e = hipMemcpyAsync(kind, d_kind.p, n * sizeof(int), hipMemcpyDeviceToHost, ds.stream);
+    if (e == hipSuccess && index) e = hipMemcpyAsync(index, d_idx.p, n * sizeof(int), hipMemcpyDeviceToHost, ds.stream);
+    const hipError_t es = hipStreamSynchronize(ds.stream);
+    if (e == hipSuccess) e = es;
+    cleanup();
+    if (e != hipSuccess) return fail(RT_ERR_DEVICE, "rt_closest_hits: %s", hipGetErrorString(e));
     return RT_OK;
 }
 

@@ -446,10 +446,8 @@ Camera create_camera(const JVal& cam, double aspect) {     // scene-loader.js:20
     const double focus = fd ? num(fd) : vlen(vsub(position, look_at));
     const JVal* ty = cam.get("type");
     std::string type = "perspective";
-    if (truthy(ty)) {
-        if (ty->t != JVal::Str) throw LoadError{"camera.type is not a string"};
-        type = ty->s;
-    }
+    if (truthy(ty))   // camera.js compares type with === only: a non-string type is neither kind
+        type = ty->t == JVal::Str ? ty->s : std::string("\x01non-string");
     const JVal* as = cam.get("aspect");
     const double final_aspect = truthy(as) ? num(as) : aspect;
     return make_camera(position, look_at, up, fov, final_aspect, aperture, focus, type);
@@ -524,6 +522,14 @@ int rt_json_scene_load(const char* json, size_t len, int32_t width, int32_t heig
             for (const JVal& o : objs->a) {
                 if (o.t == JVal::Null) throw LoadError{"object is null"};   // objData.type on null throws
                 create_object(*s, o);
+            }
+        // lights (scene-loader.js:69-76) are parsed but never rendered; _createLight calls
+        // lightData.type.toLowerCase() (:187), which throws for a truthy non-string type: the load fails
+        const JVal* lights = root.get("lights");
+        if (truthy(lights) && lights->t == JVal::Arr)
+            for (const JVal& l : lights->a) {
+                const JVal* lt = l.t == JVal::Obj ? l.get("type") : nullptr;
+                if (truthy(lt) && lt->t != JVal::Str) throw LoadError{"light.type is not a string"};
             }
         Camera c;
         if (truthy(cam)) {

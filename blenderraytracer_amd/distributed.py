@@ -82,3 +82,30 @@ class ShardedRender:
             capi.check(self.lib.rt_finalize_device(self.scene, C.byref(self.full_settings), C.c_void_p(self.sum.data_ptr()), None,
                                                    C.c_void_p(self.post.data_ptr()), C.c_void_p(self.rgba8.data_ptr()),
                                                    C.c_void_p(stream.cuda_stream)))
+
+
+class InProcessRender:
+    """The drop-in's own multi-GPU path (rt_settings.devices, what installGpuRender(rt, {devices}) runs
+    from Node): ONE process, every frame's samples split into len(devices) contiguous ranges, range k
+    traced on devices[k] by a replica of the scene, the float64 sums copied peer-to-peer over xGMI to
+    the scene's device and added in range order there, then the epilogue.  A step is one rt_render
+    call delivering the frame's RGBA8 bytes to the host (the reference's imageData)."""
+
+    def __init__(self, tracer, devices):
+        import numpy as np
+        self.tracer = tracer
+        self.devices = list(devices)
+        self.lib = capi.load_library()
+        self.scene = tracer.scene_handle()
+        self.settings = tracer.settings(devices=self.devices if len(self.devices) > 1 else None)
+        s = self.settings
+        self.n = (s.crop_w or s.width) * (s.crop_h or s.height)
+        self.rgba8 = np.zeros(self.n * 4, dtype=np.uint8)
+        self.out = capi.Output()
+        self.out.rgba8 = self.rgba8.ctypes.data_as(C.POINTER(C.c_uint8))
+        self.stats = capi.Stats()
+        self.range = (0, s.samples)
+
+    def step(self, stats=True):
+        capi.check(self.lib.rt_render(self.scene, C.byref(self.settings), C.byref(self.out), C.cast(None, capi.PROGRESS_FN), None,
+                                      C.byref(self.stats)))

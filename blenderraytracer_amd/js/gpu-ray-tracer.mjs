@@ -43,7 +43,12 @@ export function settingsOf(rt, opts = {}) {
         exposure: rt.exposure, gamma: rt.gamma,
         seed: (opts.seed || 0) >>> 0,
         precision: PRECISION[opts.precision || 'f64'],
-        batchSamples: opts.batchSamples || 0,
+        batchSamples: batchSamplesOf(rt, opts),
+        // progressive display: the frame of the samples so far goes into imageData at every progress call
+        preview: opts.preview ? 1 : 0,
+        // 'sample': every pixel adds its samples in sample order (the reference's loop order); default: the
+        // sample pool's order (faster; the RGBA8 frame can differ by one at a floor(c*255) boundary)
+        sumOrder: opts.sumOrder === 'sample' ? 1 : 0,
         accel: ACCEL[opts.accel || 'auto'],
         // multi-GPU: every sample batch split over these HIP devices (rt_settings.devices)
         devices: opts.devices ? Array.from(opts.devices) : [],
@@ -59,6 +64,19 @@ export function settingsOf(rt, opts = {}) {
         denoiseW1: Math.exp(-(1) / (2 * rt.denoiseStrength * rt.denoiseStrength)),
         denoiseW2: Math.exp(-(2) / (2 * rt.denoiseStrength * rt.denoiseStrength)),
     };
+}
+
+// Progress granularity.  The reference reports progress and repaints after every row
+// (ray-tracer.js:224-261); the GPU renders whole frames, so render() splits the samples into
+// `progressSteps` batches (default 16; opts.batchSamples overrides, 0 = one batch): after each batch
+// onProgress fires and imageData shows the frame of the samples done so far.
+export const DEFAULT_PROGRESS_STEPS = 16;
+function batchSamplesOf(rt, opts) {
+    if (opts.batchSamples !== undefined) return opts.batchSamples || 0;
+    if (!opts.intoImageData) return 0;
+    const samples = rt.antiAliasing === 'none' ? 1 : rt.samples;
+    const steps = opts.progressSteps || DEFAULT_PROGRESS_STEPS;
+    return Math.max(1, Math.ceil(samples / steps));
 }
 
 const isCancelled = () => typeof window !== 'undefined' && window && window.renderCancelled;
@@ -95,18 +113,26 @@ export function releaseGpuScene(rt) {
 export async function gpuRender(rt, onProgress, opts = {}) {
     const nat = loadNative();
     const scene = residentScene(rt, nat, opts.device || 0);
+    const st = settingsOf(rt, { preview: !!opts.intoImageData, ...opts });
+    // render() proper: the RGBA8 frame lands in this.imageData.data (full frame only), and with
+    // st.preview every progress call first copies the running frame into it (the addon does that on
+    // the main thread), so putImageData shows it like the reference's per-row repaint
+    const into = opts.intoImageData && !opts.crop && rt.imageData && rt.imageData.data.length === rt.width * rt.height * 4;
+    if (into) st.outRgba8 = rt.imageData.data;
+    else st.preview = 0;
+    const repaint = () => { if (into && rt.ctx && rt.ctx.putImageData) rt.ctx.putImageData(rt.imageData, 0, 0); };
     try {
-        const st = settingsOf(rt, opts);
-        // render() proper: the RGBA8 frame is written straight into this.imageData.data (full frame only)
-        if (opts.intoImageData && !opts.crop && rt.imageData && rt.imageData.data.length === rt.width * rt.height * 4)
-            st.outRgba8 = rt.imageData.data;
         return await nat.render(scene, st, (f) => {
+            if (st.preview) repaint();
             if (onProgress) onProgress(f);
             if (isCancelled()) nat.cancel(scene);
         });
     } catch (e) {
         if (e && e.status === -4) {                               // RT_ERR_CANCELLED
-            // keep the progressive state: render({resume: rt.checkpointState}) continues from it
+            // like the reference (ray-tracer.js:256,264): stop silently, leaving the partial frame on the
+            // canvas: imageData holds the frame of the checkpointed samples; render({resume:
+            // rt.checkpointState}) continues from them
+            if (st.preview) repaint();
             rt.checkpointState = nat.checkpoint(scene);
             return null;
         }
@@ -122,7 +148,8 @@ function blit(rt, res) {
 }
 
 // Option 1: swap the render() of a reference RayTracer instance for the GPU path.
-// opts: {seed, precision: 'f64'|'f32', accel, batchSamples, device, devices: [HIP ordinals],
+// opts: {seed, precision: 'f64'|'f32', accel, batchSamples | progressSteps (default 16), device,
+//        devices: [HIP ordinals], sumOrder: 'pool' | 'sample',
 //        keepFloatData: also read back the post-gamma Float32 frame into this.floatData}
 export function installGpuRender(rayTracer, opts = {}) {
     rayTracer.render = async function render(onProgress) {

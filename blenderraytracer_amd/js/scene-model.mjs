@@ -154,6 +154,10 @@ export function loadFromJSON(json, width, height, perm) {
         if (json.background.intensity !== undefined) world.skyIntensity = json.background.intensity;
     }
     if (Array.isArray(json.objects)) for (const o of json.objects) { const obj = createObject(o); if (obj) world.add(obj); }
+    // lights (scene-loader.js:69-76) are parsed but never rendered; _createLight calls
+    // lightData.type.toLowerCase() (:187), which throws for a truthy non-string type: the load fails
+    if (json.lights && Array.isArray(json.lights))
+        for (const l of json.lights) if (l && l.type) l.type.toLowerCase();
     const camera = json.camera ? createCamera(json.camera, width / height) : null;
     return { world, camera, newDimensions };
 }

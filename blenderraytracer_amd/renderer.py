@@ -17,7 +17,7 @@ from .scene import PackedScene, default_scene, load_from_json, setup_camera, key
 
 def settings_struct(width, height, samples, max_bounces, anti_aliasing, tone_mapping, exposure, gamma, seed,
                     crop=None, precision=capi.RT_PREC_F64, sample_range=None, batch_samples=0, denoising=False,
-                    denoise_strength=0.5, accel=capi.RT_ACCEL_AUTO, devices=None):
+                    denoise_strength=0.5, accel=capi.RT_ACCEL_AUTO, devices=None, sum_order=capi.RT_SUM_POOL):
     """rt_settings from RayTracer fields, resolving sampleCount (ray-tracer.js:201) and the string
     switches of getAntiAliasSample (:125-149) and toneMap (:151-161)."""
     s = capi.Settings()
@@ -36,6 +36,7 @@ def settings_struct(width, height, samples, max_bounces, anti_aliasing, tone_map
     s.precision = int(precision)
     s.batch_samples = int(batch_samples)
     s.accel = int(accel)
+    s.sum_order = int(sum_order)
     if devices:                 # multi-GPU sample split (rt_settings.devices)
         if len(devices) > capi.RT_MAX_DEVICES:
             raise ValueError(f"at most {capi.RT_MAX_DEVICES} devices")
@@ -51,12 +52,14 @@ def settings_struct(width, height, samples, max_bounces, anti_aliasing, tone_map
 
 
 class GpuRayTracer:
-    def __init__(self, width, height, seed=0, device=0, precision=capi.RT_PREC_F64, accel=capi.RT_ACCEL_AUTO):
+    def __init__(self, width, height, seed=0, device=0, precision=capi.RT_PREC_F64, accel=capi.RT_ACCEL_AUTO,
+                 sum_order=capi.RT_SUM_POOL):
         self.width, self.height = int(width), int(height)
         self.seed = seed
         self.device = device
         self.precision = precision
         self.accel = accel
+        self.sum_order = sum_order
         self.max_bounces, self.samples, self.gamma, self.exposure = 5, 4, 2.2, 1.0
         self.tone_mapping, self.anti_aliasing = "reinhard", "supersampling"
         self.denoising, self.denoise_strength = False, 0.5
@@ -118,7 +121,7 @@ class GpuRayTracer:
                                self.tone_mapping, self.exposure, self.gamma, self.seed, crop=crop,
                                precision=self.precision, sample_range=sample_range, batch_samples=batch_samples,
                                denoising=self.denoising, denoise_strength=self.denoise_strength, accel=self.accel,
-                               devices=devices)
+                               devices=devices, sum_order=self.sum_order)
 
     def scene_handle(self):
         lib = capi.load_library()
@@ -132,9 +135,12 @@ class GpuRayTracer:
 
     def render(self, on_progress=None, crop=None, want=("rgba8",), batch_samples=0, resume=None, devices=None):
         """RayTracer.render: fills image_data (RGBA8) and float_data (post-gamma RGBA float).
-        Returns a dict of the requested host arrays (mean, post, rgba8, segments, draws).
+        Returns a dict of the requested host arrays (mean, post, rgba8, segments, draws, preview).
         resume: a checkpoint() result to continue from (rt_render_resume).
-        devices: HIP ordinals to split every sample batch over (multi-GPU; may repeat a device)."""
+        devices: HIP ordinals to split every sample batch over (multi-GPU; may repeat a device).
+        "preview" in want (with batch_samples): image_data shows the frame of the samples done so far
+        when on_progress runs (rt_output.preview_rgba8); a cancel (on_progress returning True) then
+        leaves that frame of the checkpointed samples in image_data and raises RuntimeError(RT_ERR_CANCELLED)."""
         lib = capi.load_library()
         scene = self.scene_handle()
         st = self.settings(crop=crop, batch_samples=batch_samples, devices=devices)
@@ -156,16 +162,22 @@ class GpuRayTracer:
         if "draws" in want:
             res["draws"] = np.zeros((ch, cw), dtype=np.uint32)
             out.draws = res["draws"].ctypes.data_as(C.POINTER(C.c_uint32))
+        if "preview" in want:
+            res["preview"] = np.zeros((ch, cw, 4), dtype=np.uint8)
+            out.preview_rgba8 = res["preview"].ctypes.data_as(C.POINTER(C.c_uint8))
         stats = capi.Stats()
         cb = capi.PROGRESS_FN(lambda f, u: int(bool(on_progress(f)) if on_progress else 0))
         if resume is None:
-            capi.check(lib.rt_render(scene, C.byref(st), C.byref(out), cb, None, C.byref(stats)))
+            rc = lib.rt_render(scene, C.byref(st), C.byref(out), cb, None, C.byref(stats))
         else:
             sums, done = resume
             sums = np.ascontiguousarray(sums, dtype=np.float64)
             assert sums.size == 3 * n, "checkpoint of another frame size"
-            capi.check(lib.rt_render_resume(scene, C.byref(st), sums.ctypes.data_as(C.POINTER(C.c_double)), int(done),
-                                            C.byref(out), cb, None, C.byref(stats)))
+            rc = lib.rt_render_resume(scene, C.byref(st), sums.ctypes.data_as(C.POINTER(C.c_double)), int(done),
+                                      C.byref(out), cb, None, C.byref(stats))
+        if rc == -4 and "preview" in want and crop is None:    # cancelled: the frame of the checkpoint stays
+            self.image_data = res["preview"]
+        capi.check(rc)
         self.last_stats = stats
         if crop is None:
             self.image_data = res["rgba8"]

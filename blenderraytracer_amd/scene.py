@@ -233,6 +233,13 @@ def load_from_json(data, width, height, perm):
     if isinstance(objs, list):
         for o in objs:
             _create_object(o, world)
+    # lights (scene-loader.js:69-76) are parsed but never rendered; _createLight calls
+    # lightData.type.toLowerCase() (:187), which throws for a truthy non-string type: the load fails
+    lights = data.get("lights")
+    if isinstance(lights, list):
+        for lt in lights:
+            if isinstance(lt, dict) and truthy(lt.get("type")):
+                _js_lower(lt["type"], "light")
     camera = create_camera(cam, width / height) if truthy(cam) else None
     return world, camera, new_dims
 

@@ -27,7 +27,8 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2      /* 2: rt_settings.device_count / devices (multi-GPU sample split) */
+#define RT_ABI_VERSION 3      /* 2: rt_settings.device_count / devices (multi-GPU sample split)
+                                 3: rt_settings.sum_order, rt_output.preview_rgba8, rt_closest_hits */
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -80,6 +81,16 @@ typedef enum rt_precision { RT_PREC_F64 = 0, RT_PREC_F32 = 1 } rt_precision;
  * volume hierarchy over the spheres and one over the triangles (built by rt_scene_create) with the
  * same tie-breaking, so both give bit-identical renders.  AUTO picks BVH for large scenes. */
 typedef enum rt_accel { RT_ACCEL_AUTO = 0, RT_ACCEL_BRUTE = 1, RT_ACCEL_BVH = 2 } rt_accel;
+
+/* Order in which a pixel's sample radiances are added into its binary64 sum (the reference adds them
+ * in sample order, ray-tracer.js:202-208).  Every path decision, segment and draw count is the same in
+ * both; only the rounding of the binary64 sums differs (~1e-16 relative).
+ *   RT_SUM_POOL (default, fastest): the sample pool adds a tile's samples in the order its wave
+ *     finishes them, then the chunk partials in chunk order.  Deterministic (the same render reproduces
+ *     its bits), but an RGBA8 byte can differ from a sample-order sum by one at a floor(c*255) boundary.
+ *   RT_SUM_SAMPLE_ORDER: one lane per pixel adds samples [sample_begin, sample_end) in sample order,
+ *     exactly the reference's loop order (slower: DESIGN.md §4). */
+typedef enum rt_sum_order { RT_SUM_POOL = 0, RT_SUM_SAMPLE_ORDER = 1 } rt_sum_order;
 
 typedef struct rt_material_desc {
     int32_t type;          /* rt_material_type */
@@ -154,8 +165,10 @@ typedef struct rt_settings {
                                   A device may be listed more than once (its ranges run on separate
                                   streams).  The scene is uploaded to each listed device on first use and
                                   kept.  Equal to one device up to the order of the binary64 additions. */
-    int32_t devices[8];        /* HIP ordinals of the devices (device_count of them) */
-    int32_t _pad2;
+    int32_t devices[8];        /* HIP ordinals of the devices (device_count of them); distinct devices need
+                                  peer access to the scene's device (enabled by the library, else
+                                  RT_ERR_DEVICE) */
+    int32_t sum_order;         /* rt_sum_order */
 } rt_settings;
 
 /* Host outputs of rt_render, each optional (NULL = not wanted). n = crop_w*crop_h pixels,
@@ -167,6 +180,11 @@ typedef struct rt_output {
     uint8_t* rgba8;        /* n*4: min(255,max(0,floor(c*255))), NaN -> 0, alpha 255 (ray-tracer.js:226-252) */
     uint32_t* segments;    /* n: world.hit calls per pixel (diagnostic; enables device counting) */
     uint32_t* draws;       /* n: RNG draws per pixel (diagnostic) */
+    uint8_t* preview_rgba8;   /* n*4, progressive display (ray-tracer.js:224-241 putImageData per row): with
+                                 batch_samples > 0, before every progress() call this buffer holds the RGBA8
+                                 frame of the samples traced so far (mean over samples_done, tone map,
+                                 gamma); on cancel it keeps the last completed batch's frame, which equals
+                                 the epilogue of the checkpointed sums */
 } rt_output;
 
 typedef struct rt_stats {
@@ -232,6 +250,16 @@ int rt_trace_device(rt_scene* scene, const rt_settings* settings, double* d_sum,
  * scene provides the scratch buffer the denoise pass reads from. */
 int rt_finalize_device(rt_scene* scene, const rt_settings* settings, const double* d_sum, double* d_mean,
                        float* d_post, uint8_t* d_rgba8, void* hip_stream);
+
+/* Diagnostic (tests): World.hit for `n` rays on the scene's device — the device arithmetic of the
+ * trace kernel's closest-hit stage (brute force in World.objects order, or the BVH walk), so the
+ * BVH's bit-identity proof is checked on the instructions the GPU runs.  rays: host, n x 6 doubles
+ * (origin xyz, direction xyz; rounded to binary32 first in RT_PREC_F32).  Outputs (host, n each, any may
+ * be NULL): t (binary64 of the winning parameter, +inf when nothing is hit), kind (-1 none, 0 sphere,
+ * 1 plane, 2 box, 3 triangle), index (primitive index within its kind, in World.objects order; mesh
+ * triangles in mesh order). */
+int rt_closest_hits(rt_scene* scene, int32_t precision, int32_t accel, const double* rays, size_t n,
+                    double* t, int32_t* kind, int32_t* index);
 
 /* Request cancellation of an in-flight rt_render on `scene` (polled between sample batches). */
 int rt_cancel(rt_scene* scene);

@@ -324,6 +324,25 @@ function kats(mods) {
     return out;
 }
 
+// Loader-only cases (cases.json loader_cases): RayTracer.loadFromJSON's verdict and what the World
+// holds afterwards -> tests/golden/loader_cases.json
+function loaderCases(mods, spec) {
+    const out = { generator: 'oracle/ref_harness/run_reference.mjs --loader', cases: {} };
+    for (const c of spec.loader_cases || []) {
+        stream.select(0xFFFFFFFE, 0xFFFFFFFE);
+        const rt = new mods.RayTracer(makeCanvas(32, 24));
+        stream.select(0xFFFFFFFF, 0xFFFFFFFF);
+        const ok = rt.loadFromJSON(JSON.parse(JSON.stringify(c.scene)));
+        const cam = rt.camera;
+        out.cases[c.name] = {
+            scene: c.scene, ok, objects: rt.world.objects.length, lights: rt.world.lights.length,
+            camera: cam ? [cam.origin, cam.lowerLeftCorner, cam.horizontal, cam.vertical].map((v) => [v.x, v.y, v.z]) : null,
+            camera_type: cam ? String(cam.type) : null,
+        };
+    }
+    return out;
+}
+
 async function main() {
     const argv = process.argv.slice(2);
     const only = argv.includes('--only') ? argv[argv.indexOf('--only') + 1].split(',') : null;
@@ -336,6 +355,13 @@ async function main() {
     };
     fs.mkdirSync(OUT, { recursive: true });
     const spec = JSON.parse(fs.readFileSync(path.join(HERE, 'cases.json'), 'utf8'));
+    if (argv.includes('--loader')) {
+        const l = loaderCases(mods, spec);
+        fs.writeFileSync(path.join(OUT, 'loader_cases.json'), JSON.stringify(l, null, 1) + '\n');
+        realLog(`loader cases: ${Object.keys(l.cases).length} (${Object.values(l.cases).filter((c) => !c.ok).length} rejected)`);
+        fs.rmSync ? fs.rmSync(dir, { recursive: true, force: true }) : fs.rmdirSync(dir, { recursive: true });
+        return;
+    }
     const manifestPath = path.join(OUT, 'manifest.json');
     const manifest = fs.existsSync(manifestPath) ? JSON.parse(fs.readFileSync(manifestPath, 'utf8')) : { cases: {} };
     manifest.generator = 'oracle/ref_harness/run_reference.mjs';

@@ -32,9 +32,11 @@ if "TCP_TOTAL_CACHE_ACCESSES_sum" in v and "TCP_TCC_READ_REQ_sum" in v:
     print(f"L1 hit rate              {1 - v['TCP_TCC_READ_REQ_sum'] / v['TCP_TOTAL_CACHE_ACCESSES_sum']:.3f}")
 if "TCC_HIT_sum" in v and "TCC_MISS_sum" in v:
     print(f"L2 hit rate              {v['TCC_HIT_sum'] / (v['TCC_HIT_sum'] + v['TCC_MISS_sum']):.3f}")
+# GRBM_GUI_ACTIVE as rocprofv3 reports it is the SUM over the 8 XCDs (MI355X_MICROARCH.md, DVFS note):
+# one XCD's busy cycles are GRBM_GUI_ACTIVE / 8, so a per-CU fraction divides by 256 x GRBM / 8
 if "GRBM_GUI_ACTIVE" in v:
     for k in ("TA_TA_BUSY_sum", "TD_TD_BUSY_sum", "TA_ADDR_STALLED_BY_TC_CYCLES_sum", "TA_DATA_STALLED_BY_TC_CYCLES_sum",
               "TCP_PENDING_STALL_CYCLES_sum", "TCP_READ_TAGCONFLICT_STALL_CYCLES_sum", "TCP_TCR_TCP_STALL_CYCLES_sum",
               "TD_TC_STALL_sum"):
         if k in v:
-            print(f"{k} per CU-cycle  {v[k] / (256 * v['GRBM_GUI_ACTIVE']):.3f}")
+            print(f"{k} per CU-cycle  {v[k] / (256 * v['GRBM_GUI_ACTIVE'] / 8):.3f}")

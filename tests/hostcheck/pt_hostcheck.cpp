@@ -170,17 +170,12 @@ extern "C" long long ptc_away_check(long long n, unsigned seed, long long* taken
     return bad;
 }
 
-// BVH stress: n random rays per scene, closest_hit (World order) vs closest_hit_bvh.  Rays start at
-// random points and aim at random primitives' surfaces (near-tangent for spheres, near edges and
-// vertices for triangles) to exercise the conservative node bounds.  Returns the number of rays
-// whose (t, primitive kind, index) differ.
-extern "C" long long ptc_bvh_check(const rt_scene_desc* d, long long n, unsigned seed, long long* hits) {
-    HostView<double> hv;
-    if (!hv.init(d)) return -1;
-    const SceneView<double>& v = hv.v;
+// BVH stress rays: n random rays per scene that start at random points and aim at random primitives'
+// surfaces (near-tangent for spheres, near edges and vertices for triangles) to exercise the
+// conservative node bounds.  Writes up to n rays (origin xyz, direction xyz) into rays; returns the count.
+static long long bvh_rays(const HostScene& hs, long long n, unsigned seed, double* rays) {
     std::mt19937_64 gen(seed);
     std::uniform_real_distribution<double> U(-1.0, 1.0);
-    const HostScene& hs = hv.hs;
     const int ns = (int)hs.sphere_r.size(), nt = (int)hs.tri_mat.size();
     double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
     for (int i = 0; i < ns; ++i)
@@ -193,7 +188,7 @@ extern "C" long long ptc_bvh_check(const rt_scene_desc* d, long long n, unsigned
             lo[a] = std::min(lo[a], hs.tri_verts[3 * i + a]);
             hi[a] = std::max(hi[a], hs.tri_verts[3 * i + a]);
         }
-    long long bad = 0, nh = 0;
+    long long m = 0;
     for (long long it = 0; it < n; ++it) {
         double o[3], target[3];
         for (int a = 0; a < 3; ++a) o[a] = lo[a] + (hi[a] - lo[a]) * (0.5 + 0.75 * U(gen));
@@ -216,7 +211,45 @@ extern "C" long long ptc_bvh_check(const rt_scene_desc* d, long long n, unsigned
             continue;
         }
         const double dl = std::pow(10.0, 2.0 * U(gen));
-        V3<double> O{o[0], o[1], o[2]}, D{(target[0] - o[0]) * dl, (target[1] - o[1]) * dl, (target[2] - o[2]) * dl};
+        double* r = rays + 6 * m++;
+        for (int a = 0; a < 3; ++a) {
+            r[a] = o[a];
+            r[3 + a] = (target[a] - o[a]) * dl;
+        }
+    }
+    return m;
+}
+
+// The stress rays of bvh_rays for the device test (tests/test_gpu_parity.py runs them through
+// rt_closest_hits) with the host's World-order closest hit of the first host_n: t (+inf on a miss), kind,
+// index.
+extern "C" long long ptc_bvh_rays(const rt_scene_desc* d, long long n, unsigned seed, long long host_n, double* rays,
+                                  double* t, int* kind, int* idx) {
+    HostView<double> hv;
+    if (!hv.init(d)) return -1;
+    const long long m = bvh_rays(hv.hs, n, seed, rays);
+    for (long long k = 0; k < std::min(m, host_n); ++k) {
+        const double* r = rays + 6 * k;
+        const Closest<double> a = closest_hit<double>(hv.v, V3<double>{r[0], r[1], r[2]}, V3<double>{r[3], r[4], r[5]});
+        t[k] = a.kind == HIT_NONE ? INFINITY : a.t;
+        kind[k] = a.kind;
+        idx[k] = a.kind == HIT_NONE ? -1 : a.idx;
+    }
+    return m;
+}
+
+// BVH stress on the host: closest_hit (World order) vs closest_hit_bvh (both walks) on the bvh_rays.
+// Returns the number of rays whose (t, primitive kind, index) differ.
+extern "C" long long ptc_bvh_check(const rt_scene_desc* d, long long n, unsigned seed, long long* hits) {
+    HostView<double> hv;
+    if (!hv.init(d)) return -1;
+    const SceneView<double>& v = hv.v;
+    std::vector<double> rays(6 * (size_t)std::max(0LL, n));
+    const long long m = bvh_rays(hv.hs, n, seed, rays.data());
+    long long bad = 0, nh = 0;
+    for (long long it = 0; it < m; ++it) {
+        const double* r = &rays[6 * it];
+        V3<double> O{r[0], r[1], r[2]}, D{r[3], r[4], r[5]};
         const Closest<double> a = closest_hit<double>(v, O, D);
         Work w{0, 0, 0};
         int stack[RT_BVH_STACK];

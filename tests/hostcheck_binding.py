@@ -35,6 +35,9 @@ def _bind(L):
     L.ptc_bvh_info.argtypes = [C.POINTER(capi.SceneDesc)] + [C.POINTER(C.c_int)] * 4
     L.ptc_away_check.argtypes = [C.c_longlong, C.c_uint, C.POINTER(C.c_longlong)]
     L.ptc_away_check.restype = C.c_longlong
+    L.ptc_bvh_rays.argtypes = [C.POINTER(capi.SceneDesc), C.c_longlong, C.c_uint, C.c_longlong, C.POINTER(C.c_double),
+                               C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.ptc_bvh_rays.restype = C.c_longlong
     return L
 
 
@@ -66,6 +69,22 @@ def bvh_check(packed, n, seed):
     bad = lib().ptc_bvh_check(C.byref(packed.desc), n, seed, C.byref(hits))
     assert bad >= 0
     return bad, hits.value
+
+
+def bvh_rays(packed, n, seed, host_n=None):
+    """The BVH stress rays (n x 6 float64: origin, direction) and the host's World-order closest hit
+    (t, kind, index) of the first host_n of them (default all) — the kernel's own code compiled for the
+    CPU."""
+    host_n = n if host_n is None else host_n
+    rays = np.zeros((n, 6))
+    t = np.full(n, np.nan)
+    kind = np.full(n, -2, dtype=np.int32)
+    idx = np.full(n, -2, dtype=np.int32)
+    m = lib().ptc_bvh_rays(C.byref(packed.desc), n, seed, host_n, rays.ctypes.data_as(C.POINTER(C.c_double)),
+                           t.ctypes.data_as(C.POINTER(C.c_double)), kind.ctypes.data_as(C.POINTER(C.c_int)),
+                           idx.ctypes.data_as(C.POINTER(C.c_int)))
+    assert m >= 0
+    return rays[:m], t[:m], kind[:m], idx[:m]
 
 
 def render(packed, settings, L=None):

@@ -83,6 +83,31 @@ if (cmd === 'pack') {
         const a = full.imageData.data, b = part.imageData.data;
         summary._resume = { samplesDone: done, equal: a.length === b.length && a.every((v, i) => v === b[i]) };
     }
+    // progressive display (ray-tracer.js:224-264): render() splits the samples into 16 batches, and at
+    // every progress call imageData already holds the frame of the samples done so far; a cancel
+    // leaves the frame of the checkpointed samples (the batch in flight completes)
+    {
+        const { rt: pr } = tracerFor('kitchen_sink');
+        pr.updateRenderSettings({ samples: 32 });
+        const seen = [], frames = [];
+        await pr.render((f) => { seen.push(f); frames.push(Buffer.from(pr.imageData.data).toString('base64')); });
+        const final = Buffer.from(pr.imageData.data).toString('base64');
+        const { rt: pc } = tracerFor('kitchen_sink');
+        pc.updateRenderSettings({ samples: 32 });
+        global.window = { renderCancelled: false };
+        let calls = 0;
+        await pc.render(() => { if (++calls === 5) global.window.renderCancelled = true; });
+        global.window.renderCancelled = false;
+        const done = pc.checkpointState ? pc.checkpointState.samplesDone : -1;
+        const { rt: pref } = tracerFor('kitchen_sink', { batchSamples: 2 });
+        pref.updateRenderSettings({ samples: done > 0 ? done : 1 });
+        await pref.render();
+        const a = pc.imageData.data, b = pref.imageData.data;
+        summary._progressive = {
+            progress: seen, distinctFrames: new Set(frames).size, lastFrameFinal: frames[frames.length - 1] === final,
+            cancelDone: done, cancelFrameEqual: a.length === b.length && a.every((v, i) => v === b[i]),
+        };
+    }
     // multi-GPU through the drop-in: settings.devices = [0, 0] (two sample ranges on this GPU), and
     // the scene upload cached across render() calls
     {
@@ -108,6 +133,17 @@ if (cmd === 'pack') {
         };
     }
     fs.writeFileSync(path.join(outdir, 'summary.json'), JSON.stringify(summary));
+} else if (cmd === 'loadcheck') {
+    // GpuRayTracer.loadFromJSON (scene-model.mjs) on the reference's loader-only fixtures
+    const cases = JSON.parse(fs.readFileSync(path.join(REPO, 'tests', 'golden', 'loader_cases.json'), 'utf8')).cases;
+    const out = {};
+    for (const [name, c] of Object.entries(cases)) {
+        const rt = new GpuRayTracer({ width: 32, height: 24 }, { seed: 1 });
+        const ok = rt.loadFromJSON(JSON.parse(JSON.stringify(c.scene)));
+        const cam = rt.camera;
+        out[name] = { ok, camera: [cam.origin, cam.lowerLeftCorner, cam.horizontal, cam.vertical].map((v) => [v.x, v.y, v.z]) };
+    }
+    process.stdout.write(JSON.stringify(out));
 } else if (cmd === 'refpack') {
     // The drop-in: the reference's own RayTracer (temp copy prepared by the caller), its render()
     // swapped for the GPU one; here only its packing is compared (no GPU in the build container).

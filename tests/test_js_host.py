@@ -113,10 +113,21 @@ def test_js_packing_of_real_reference_objects():
         shutil.rmtree(d, ignore_errors=True)
 
 
+def test_js_loader_cases_match_reference():
+    """GpuRayTracer.loadFromJSON (scene-model.mjs) against the reference's loader-only fixtures
+    (tests/golden/loader_cases.json): same verdict, and the same camera vectors when it loads."""
+    ref = json.load(open(os.path.join(ROOT, "tests", "golden", "loader_cases.json")))["cases"]
+    out = json.loads(run_tool("loadcheck"))
+    for name, c in ref.items():
+        assert out[name]["ok"] == c["ok"], name
+        if c["ok"]:
+            assert out[name]["camera"] == c["camera"], name
+
+
 def test_addon_loads_without_gpu_and_fails_loudly():
     if not os.path.exists(ADDON):
         pytest.skip("rt_napi.node not built")
-    code = ("const m=require(%r); if (m.abiVersion()!==2) process.exit(3);"
+    code = ("const m=require(%r); if (m.abiVersion()!==3) process.exit(3);"
             "if (m.deviceCount()===0) { try { m.createScene({camera:new Float64Array(22),perm:new Int32Array(512)},0);"
             " process.exit(4);} catch(e) { if(!/no HIP device/.test(e.message)) process.exit(5);} }") % ADDON
     r = subprocess.run([NODE, "-e", code], capture_output=True)
@@ -141,7 +152,7 @@ def test_js_gpu_render_matches_reference(gpu):
             assert np.array_equal(np.isnan(mean), np.isnan(lin))
             ok = ~np.isnan(lin)
             assert np.all(np.abs(mean[ok] - lin[ok]) <= 1e-12 * np.maximum(1, np.abs(lin[ok]))), name
-            assert np.mean(ld("rgba8", np.uint8).reshape(ch, cw, 4) == gc.load_array(name, "rgba8")) >= 0.9999
+            assert np.array_equal(ld("rgba8", np.uint8).reshape(ch, cw, 4), gc.load_array(name, "rgba8")), name
         r = summary["_render"]
         assert r["progress"][-1] == 1.0 and r["nonzero"]
         assert summary["_floatData"] == {"absentByDefault": True, "kept": True, "rgbaEqual": True}
@@ -155,6 +166,11 @@ def test_js_gpu_render_matches_reference(gpu):
         assert dv["segsEqual"] and dv["drawsEqual"] and dv["maxRel"] <= 1e-13, dv
         assert dv["sceneCached"] and dv["reuploaded"], dv
         assert summary["_resume"]["samplesDone"] in (4, 6, 8)
+        pg = summary["_progressive"]                # default 16 progress batches, preview frames, cancel
+        assert len(pg["progress"]) >= 16 and pg["progress"][-1] == 1.0, pg["progress"]
+        assert all(x < y for x, y in zip(pg["progress"], pg["progress"][1:])), pg["progress"]
+        assert pg["distinctFrames"] >= 8 and pg["lastFrameFinal"], pg
+        assert pg["cancelDone"] == 12 and pg["cancelFrameEqual"], pg
 
 
 def test_pow5_vs_v8_math_pow(tmp_path):

@@ -163,3 +163,26 @@ def test_json_parser_details():
     d = js.desc()
     assert d.objects[0].type == capi.RT_OBJ_SPHERE and list(d.objects[0].g)[:4] == [1.0, -5.0, 0.25, 0.75]
     js.close()
+
+
+LOADER_CASES = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "loader_cases.json")))["cases"]
+
+
+@pytest.mark.parametrize("name", sorted(LOADER_CASES))
+def test_loader_cases_match_reference(name):
+    """Loader-only fixtures from the REAL reference (oracle/ref_harness/run_reference.mjs --loader):
+    RayTracer.loadFromJSON's verdict on each scene — e.g. a light whose `type` is a truthy non-string
+    makes _createLight's type.toLowerCase() throw (scene-loader.js:187) and the load fail, while a
+    non-string camera type loads (camera.js compares it with === only) — and, when it loads, the
+    camera vectors bit for bit.  Both the Python host and the C++ loader (check_same: they also agree
+    with each other object by object) must give the reference's verdict."""
+    c = LOADER_CASES[name]
+    err = check_same(json.dumps(c["scene"]), 32, 24, 1)
+    assert (err is None) == c["ok"], (name, err)
+    if c["ok"]:
+        rt = GpuRayTracer(32, 24, seed=1)
+        assert rt.load_from_json(c["scene"])
+        cam = rt.packed().desc.camera
+        got = [list(cam.origin), list(cam.lower_left), list(cam.horizontal), list(cam.vertical)]
+        assert got == c["camera"], name
+        assert cam.type == (capi.RT_CAM_ORTHOGRAPHIC if c["camera_type"] == "orthographic" else capi.RT_CAM_PERSPECTIVE)
