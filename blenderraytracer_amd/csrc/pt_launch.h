@@ -34,7 +34,7 @@ hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Cou
 // the sample pool's split of `ns` samples of a cw x ch crop: 8x8 tiles, samples per chunk, chunks and the
 // bytes of all chunk partials of one launch
 struct PoolPlan { int tiles, chunk, chunks; size_t part_bytes; };
-PoolPlan pool_plan(int cw, int ch, int ns, bool tri_bvh);
+PoolPlan pool_plan(int cw, int ch, int ns, bool tri_bvh, int chunk = 0);
 // the pool kernel writing every chunk (even one) into `part` (>= pool_plan(..).part_bytes), sums untouched:
 // batches may trace concurrently on several streams; launch_reduce then adds part to sum in chunk order
 template <class R>
@@ -53,7 +53,7 @@ bool trace_uses_pool();
 // scratch bytes the sample pool needs to trace `ns` samples of a cw x ch crop in one launch (0: one
 // chunk, the partials go straight to the sums).  With less scratch (but at least one chunk's worth,
 // tiles x kPartialBytesPerTile) launch_trace splits the samples over several launches.
-size_t pool_partial_bytes(int cw, int ch, int ns, bool tri_bvh);
+size_t pool_partial_bytes(int cw, int ch, int ns, bool tri_bvh, int chunk = 0);
 
 // dst[i] += src[i] (n elements, both on the stream's device): merging the shards of a multi-device render
 template <class T>

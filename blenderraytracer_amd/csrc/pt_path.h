@@ -20,6 +20,7 @@ struct ImageParams {
     int max_depth;
     int aa_mode;
     uint32_t seedm;            // seed_mix(seed)
+    int pool_chunk;            // samples per sample-pool wave (0: pool_chunk's rule for this launch's samples)
 };
 
 // Stochastic AA offsets (ray-tracer.js:136-141): sqrt, cos and sin in binary64 are long code that

@@ -305,9 +305,9 @@ static size_t stack_lds_bytes(const SceneView<R>& sc) {
 
 static int crop_tiles(int cw, int ch) { return ((cw + 7) / 8) * ((ch + 7) / 8); }
 
-size_t pool_partial_bytes(int cw, int ch, int ns, bool tri_bvh) {
+size_t pool_partial_bytes(int cw, int ch, int ns, bool tri_bvh, int chunk_override) {
     if (cw <= 0 || ch <= 0 || ns <= 0) return 0;
-    const int tiles = crop_tiles(cw, ch), chunk = pool_chunk(ns, tiles, tri_bvh);
+    const int tiles = crop_tiles(cw, ch), chunk = chunk_override > 0 ? chunk_override : pool_chunk(ns, tiles, tri_bvh);
     const size_t chunks = (size_t)((ns + chunk - 1) / chunk);
     return chunks > 1 ? chunks * tiles * kPartialBytesPerTile : 0;
 }
@@ -327,7 +327,7 @@ static hipError_t launch_pool(const TraceArgs<R>& a0, bool count, hipStream_t st
     // the chunk choice depends on the scene, not on the walk, so BVH and brute force add the samples
     // in the same order (bit-identical sums)
     const bool tri_bvh = a0.sc.num_tri_nodes > 0;
-    const int tiles = crop_tiles(im.cw, im.ch), chunk = pool_chunk(ns_all, tiles, tri_bvh);
+    const int tiles = crop_tiles(im.cw, im.ch), chunk = im.pool_chunk > 0 ? im.pool_chunk : pool_chunk(ns_all, tiles, tri_bvh);
     const int chunks_all = (ns_all + chunk - 1) / chunk;
     // chunk partials that fit the scratch buffer; a frame that needs more is split into launches
     const size_t per_chunk = (size_t)tiles * kPartialBytesPerTile;
@@ -388,11 +388,11 @@ hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Cou
 template hipError_t launch_trace<double>(const SceneView<double>&, const ImageParams&, const Counters&, bool, bool, hipStream_t);
 template hipError_t launch_trace<float>(const SceneView<float>&, const ImageParams&, const Counters&, bool, bool, hipStream_t);
 
-PoolPlan pool_plan(int cw, int ch, int ns, bool tri_bvh) {
+PoolPlan pool_plan(int cw, int ch, int ns, bool tri_bvh, int chunk) {
     PoolPlan p{0, 0, 0, 0};
     if (cw <= 0 || ch <= 0 || ns <= 0) return p;
     p.tiles = crop_tiles(cw, ch);
-    p.chunk = pool_chunk(ns, p.tiles, tri_bvh);
+    p.chunk = chunk > 0 ? chunk : pool_chunk(ns, p.tiles, tri_bvh);
     p.chunks = (ns + p.chunk - 1) / p.chunk;
     p.part_bytes = (size_t)p.chunks * p.tiles * kPartialBytesPerTile;
     return p;
@@ -412,7 +412,7 @@ template <class R>
 hipError_t launch_trace_partials(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh,
                                  double* part, size_t part_bytes, hipStream_t stream) {
     if (im.cw <= 0 || im.ch <= 0 || im.s_end <= im.s_begin) return hipSuccess;
-    const PoolPlan p = pool_plan(im.cw, im.ch, im.s_end - im.s_begin, sc.num_tri_nodes > 0);
+    const PoolPlan p = pool_plan(im.cw, im.ch, im.s_end - im.s_begin, sc.num_tri_nodes > 0, im.pool_chunk);
     if (!part || part_bytes < p.part_bytes) return hipErrorInvalidValue;
     TraceArgs<R> a{sc, im, c};
     const bool count = c.segs || c.draws;
@@ -428,7 +428,7 @@ template hipError_t launch_trace_partials<float>(const SceneView<float>&, const 
 
 hipError_t launch_reduce(const ImageParams& im, double* sum, const double* part, bool tri_bvh, hipStream_t stream) {
     if (im.cw <= 0 || im.ch <= 0 || im.s_end <= im.s_begin) return hipSuccess;
-    const PoolPlan p = pool_plan(im.cw, im.ch, im.s_end - im.s_begin, tri_bvh);
+    const PoolPlan p = pool_plan(im.cw, im.ch, im.s_end - im.s_begin, tri_bvh, im.pool_chunk);
     hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((p.tiles + 3) / 4)), dim3(256), 0, stream, im, sum, part, p.tiles,
                        p.chunks);
     return hipGetLastError();

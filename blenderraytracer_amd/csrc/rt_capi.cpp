@@ -387,9 +387,10 @@ hipError_t scratch_idle(DeviceState& ds) {
     return ds.scratch_used ? hipEventSynchronize(ds.scratch_ev) : hipSuccess;
 }
 
-int ensure_partials(const rt_scene* sc, DeviceState& ds, int cw, int ch, int samples, bool pool, Counters& c) {
+int ensure_partials(const rt_scene* sc, DeviceState& ds, int cw, int ch, int samples, bool pool, Counters& c,
+                    int chunk = 0) {
     if (!pool || samples <= 0 || cw <= 0 || ch <= 0) return RT_OK;
-    const size_t want_all = pool_partial_bytes(cw, ch, samples, sc->tri_bvh);
+    const size_t want_all = pool_partial_bytes(cw, ch, samples, sc->tri_bvh, chunk);
     if (want_all == 0) return RT_OK;
     const size_t per_chunk = (size_t)((cw + 7) / 8) * ((ch + 7) / 8) * kPartialBytesPerTile;
     size_t want = want_all;
@@ -675,7 +676,21 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     DeviceState& h = sc->home;
     const bool want_preview = out && out->preview_rgba8 && nb > 1;
     std::vector<Counters> cs(nsh);
-    bool overlap = pool && nb > 1 && s->max_depth > 0;
+    // Several batches: every batch's pool waves take min(batch, chunk) samples, chunk being the pool's
+    // rule for the shard's whole share of the render (not for one batch: short chunks lengthen each
+    // wave's drain relative to its work).  The same batches give the same chunks on a resume (the share
+    // is counted from sample_begin), so a resumed render stays bit-identical.
+    std::vector<int> chunk_hint(nsh, 0);
+    if (pool && nb > 1)
+        for (int k = 0; k < nsh; ++k) {
+            int a, b;
+            shard_range(base, s1, k, nsh, a, b);
+            chunk_hint[k] = pool_plan(cw, ch, std::max(1, b - a), sc->tri_bvh).chunk;
+        }
+    auto batch_chunk = [&](int k, int ns) { return chunk_hint[k] > 0 ? std::max(1, std::min(chunk_hint[k], ns)) : 0; };
+    // overlapped batches: the pool with several batches.  Not with per-pixel counters over several
+    // devices: the trace kernels add those directly, and a replica's merge zeroes them between batches
+    bool overlap = pool && nb > 1 && s->max_depth > 0 && !(nsh > 1 && (want_segs || want_draws));
     for (int k = 0; k < nsh; ++k) {
         DeviceState& ds = *states[k];
         HIP_TRY(hipSetDevice(ds.device));
@@ -683,7 +698,8 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         HIP_TRY(ds.total.ensure(kTotalSlots));
         int b0, b1;
         shard_range(s0, s0 + std::min(batch, s1 - s0), k, nsh, b0, b1);
-        if (overlap) overlap = ensure_overlap_partials(ds, pool_plan(cw, ch, std::max(1, b1 - b0), sc->tri_bvh).part_bytes);
+        const int ns = std::max(1, b1 - b0);
+        if (overlap) overlap = ensure_overlap_partials(ds, pool_plan(cw, ch, ns, sc->tri_bvh, batch_chunk(k, ns)).part_bytes);
     }
     for (int k = 0; k < nsh; ++k) {
         DeviceState& ds = *states[k];
@@ -692,7 +708,8 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         c = Counters{ds.sum.p, nullptr, nullptr, ds.total.p};
         int b0, b1;
         shard_range(s0, s0 + std::min(batch, s1 - s0), k, nsh, b0, b1);
-        if (!overlap && s->max_depth > 0 && (rc = ensure_partials(sc, ds, cw, ch, std::max(1, b1 - b0), pool, c))) return rc;
+        const int ns = std::max(1, b1 - b0);
+        if (!overlap && s->max_depth > 0 && (rc = ensure_partials(sc, ds, cw, ch, ns, pool, c, batch_chunk(k, ns)))) return rc;
         HIP_TRY(order_scratch(ds, ds.stream));
         if (sums_in && &ds == &h)
             HIP_TRY(hipMemcpyAsync(ds.sum.p, sums_in, 3 * n * sizeof(double), hipMemcpyHostToDevice, ds.stream));
@@ -755,6 +772,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
             DeviceState& ds = *states[k];
             ImageParams bi = im;
             shard_range(b, be, k, nsh, bi.s_begin, bi.s_end);
+            bi.pool_chunk = batch_chunk(k, bi.s_end - bi.s_begin);
             HIP_TRY(hipSetDevice(ds.device));
             if (overlap) HIP_TRY(trace_overlapped(sc, ds, s, bi, cs[k], kb % 2, kb >= 2));
             else HIP_TRY(trace(sc, ds, s, bi, cs[k], ds.stream));
@@ -762,7 +780,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         int r;
         if (nsh > 1 && (r = merge_shards(sc, states, n, want_segs, want_draws))) return r;
         HIP_TRY(hipSetDevice(h.device));
-        if (want_preview) {                       // the running frame: mean over the samples so far
+        if (want_preview && be < s1) {            // the running frame: mean over the samples so far
             FinalizeParams fp{(int)n, be - base, s->tone_map, s->exposure, s->gamma};
             HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview.p, h.stream));
             HIP_TRY(hipMemcpyAsync(sc->preview_host[kb % 2], sc->preview.p, 4 * n, hipMemcpyDeviceToHost, h.stream));
@@ -775,7 +793,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         HIP_TRY(hipEventSynchronize(sc->batch_done[kb % 2]));
         const int be = std::min(s1, s0 + (kb + 1) * batch);
         sc->ckpt_done = be;
-        if (want_preview) memcpy(out->preview_rgba8, sc->preview_host[kb % 2], 4 * n);
+        if (want_preview && be < s1) memcpy(out->preview_rgba8, sc->preview_host[kb % 2], 4 * n);
         return RT_OK;
     };
     int status = RT_OK, enqueued = 0;
@@ -793,7 +811,8 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         if (progress && be < s1 && progress((double)(be - s0) / (double)(s1 - s0), user)) sc->cancel.store(1);
         if (sc->cancel.load()) {
             if (enqueued > kb + 1 && (status = complete(kb + 1))) break;   // the batch in flight finishes
-            status = fail(RT_ERR_CANCELLED, "render cancelled after %d samples", sc->ckpt_done);
+            // ... and if it was the last one, the render has completed
+            if (sc->ckpt_done < s1) status = fail(RT_ERR_CANCELLED, "render cancelled after %d samples", sc->ckpt_done);
             break;
         }
     }

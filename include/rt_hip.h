@@ -181,10 +181,11 @@ typedef struct rt_output {
     uint32_t* segments;    /* n: world.hit calls per pixel (diagnostic; enables device counting) */
     uint32_t* draws;       /* n: RNG draws per pixel (diagnostic) */
     uint8_t* preview_rgba8;   /* n*4, progressive display (ray-tracer.js:224-241 putImageData per row): with
-                                 batch_samples > 0, before every progress() call this buffer holds the RGBA8
-                                 frame of the samples traced so far (mean over samples_done, tone map,
-                                 gamma); on cancel it keeps the last completed batch's frame, which equals
-                                 the epilogue of the checkpointed sums */
+                                 more than one sample batch, before every progress() call this buffer holds
+                                 the RGBA8 frame of the samples traced so far (mean over those samples, tone
+                                 map, gamma; no denoise, like the reference's rows before its final pass).
+                                 A cancel is observed after a batch, the batch already in flight completes,
+                                 and the buffer then holds the frame of the checkpointed samples */
 } rt_output;
 
 typedef struct rt_stats {
@@ -217,7 +218,9 @@ void rt_scene_destroy(rt_scene* scene);
 /* Full render into host buffers: trace, finalize (tone map, gamma, RGBA8) and copy back.
  * Replaces RayTracer.render (ray-tracer.js:166-281) minus the DOM. Synchronous.
  * progress(fraction, user) is called between sample batches from the calling thread; a non-zero
- * return value cancels (like window.renderCancelled, ray-tracer.js:190,196).
+ * return value cancels (like window.renderCancelled, ray-tracer.js:190,196).  Batches are pipelined
+ * (the next one is queued on the GPU before the host waits for the current one), so a cancel takes
+ * effect after the batch in flight; RT_ERR_CANCELLED unless that was the last batch.
  * Threading: one call in flight per scene (rt_render, rt_render_resume, rt_trace_device,
  * rt_finalize_device, rt_render_checkpoint), as for the reference's render(); calls on different
  * scenes may run concurrently from different threads.  Asynchronous device calls on different streams
