@@ -240,9 +240,12 @@ def node_end_to_end(cfg, args):
         os.unlink(path)
     return {"value": round(out["value"], 3), "unit": "Msamples/s", "wall_ms": round(out["wall_ms"], 3),
             "first_call_ms": round(out["first_call_ms"], 3), "kernel_ms": out["kernel_ms"],
+            "progress_calls": out.get("progress_calls"), "one_batch_wall_ms": out.get("one_batch_wall_ms"),
             "what": "GpuRayTracer.render() from Node (the installGpuRender path): scene resident from the first call "
-                    "(first_call_ms includes its upload and BVH build), pack + compare, trace, epilogue, RGBA8 "
-                    "readback into imageData (what the reference's render() produces)"}
+                    "(first_call_ms includes its upload and BVH build), pack + compare, trace in 16 progressive "
+                    "sample batches (onProgress + the running frame in imageData after each), epilogue, RGBA8 "
+                    "into imageData (what the reference's render() produces); one_batch_wall_ms: the same frame "
+                    "as one batch"}
 
 
 def build_provenance():

@@ -17,10 +17,23 @@ const ms = () => Number(process.hrtime.bigint()) * 1e-6;
     let t = ms();
     await rt.render();
     const first = ms() - t;
+    const progress = [];
     t = ms();
-    await rt.render();
+    await rt.render((f) => progress.push(f));
     const wall = ms() - t;
+    const kernel = rt.lastStats ? rt.lastStats.kernelMs : null;
+    // the same frame as ONE sample batch (no progress calls, no preview frames): what the default
+    // 16-batch progressive render costs over it
+    const one = new GpuRayTracer({ width: a.width, height: a.height }, { seed: a.seed, precision: a.precision || 'f64', batchSamples: 0 });
+    one.loadFromJSON(JSON.parse(fs.readFileSync(a.scene, 'utf8')));
+    if (one.width !== a.width || one.height !== a.height) one.resizeCanvas(a.width, a.height);
+    one.updateRenderSettings({ samples: a.spp, maxBounces: a.depth });
+    await one.render();
+    t = ms();
+    await one.render();
+    const wallOne = ms() - t;
     const n = a.width * a.height * a.spp;
     process.stdout.write(JSON.stringify({ value: n / (wall * 1e-3) / 1e6, wall_ms: wall, first_call_ms: first,
-                                          kernel_ms: rt.lastStats ? rt.lastStats.kernelMs : null }) + '\n');
+                                          kernel_ms: kernel, progress_calls: progress.length,
+                                          one_batch_wall_ms: wallOne }) + '\n');
 })().catch((e) => { process.stderr.write(String(e.stack || e) + '\n'); process.exit(1); });
