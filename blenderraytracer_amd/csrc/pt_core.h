@@ -649,7 +649,10 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
         if (sc.num_sphere_nodes > 0)
             bvh_walk<WIDE>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w, leaf);
     }
-    if (sc.num_tri_nodes > 0) {
+#ifndef RT_NO_TRI
+#define RT_NO_TRI 0
+#endif
+    if (!RT_NO_TRI && sc.num_tri_nodes > 0) {
         auto leaf = [&](int fc) { tri_leaf(sc, fc, o, d, tmin, b, tl, w); };
         bvh_walk<WIDE>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, leaf);
     }

@@ -137,13 +137,34 @@ void trace_kernel(const TraceArgs<R> args) {
 // directly.  Against the in-order lane-per-pixel kernel only the order of the binary64 additions
 // differs (tests/test_gpu_parity.py::test_sample_pool_vs_lane_per_pixel: <= 1e-13 relative, every
 // segment and draw count identical).
+// RT_PARK (binary64 BVH walk): the path state the walk never reads — the throughput T, depth, the
+// sample's segment count, its pixel m, the RNG key and draw count, the lane's segment total — is kept
+// in LDS across closest_hit_acc instead of in VGPRs, and the walk's stack is sized to the scene's
+// deepest leaf (dynamic LDS), so that the kernel fits RT_BVH_WAVES_PER_SIMD waves per SIMD.
+#ifndef RT_PARK
+#define RT_PARK 0
+#endif
+constexpr int kParkDoubles = 3, kParkInts = 6;
+template <class R, int ACC>
+constexpr bool parks() { return RT_PARK != 0 && sizeof(R) == 8 && ACC >= ACC_BVH_STACK; }
+
 template <class R, bool COUNT, int ACC>
 __global__ __launch_bounds__(64, (waves_per_simd<R, ACC>()))
 void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const int tiles, const int chunk) {
     const ImageParams& im = args.im;
     const SceneView<R>& sc = args.sc;
+    constexpr bool PARK = parks<R, ACC>();
     BvhStack stk{nullptr, 0};
-    if constexpr (ACC >= ACC_BVH_STACK) {
+    double* park_d = nullptr;
+    uint32_t* park_i = nullptr;
+    if constexpr (PARK) {
+        // dynamic LDS: [3 x 64 doubles][6 x 64 dwords][stack_entries x 64 ints]
+        extern __shared__ double park_dyn[];
+        park_d = park_dyn + threadIdx.x;
+        park_i = reinterpret_cast<uint32_t*>(park_dyn + kParkDoubles * 64) + threadIdx.x;
+        stk.base = reinterpret_cast<int*>(park_dyn + kParkDoubles * 64) + kParkInts * 64 + threadIdx.x;
+        stk.stride = 64;
+    } else if constexpr (ACC >= ACC_BVH_STACK) {
         // per-lane traversal stacks, entry k of lane t at [k * 64 + t]: RT_BVH_STACK (binary64) or
         // sc.stack_entries (binary32: dynamic LDS sized by the launch to the scene's deepest leaf) x 4 B
         if constexpr (sizeof(R) == 8) {
@@ -194,7 +215,20 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
     if (live) begin_item((uint32_t)lane);
     while (live) {                            // lanes only ever leave this loop, so every live lane
         const uint64_t t0 = RT_TICK();        // has seen every update of `next`
+        if constexpr (PARK) {
+            park_d[0] = (double)T.x; park_d[64] = (double)T.y; park_d[128] = (double)T.z;
+            park_i[0] = (uint32_t)depth; park_i[64] = isegs; park_i[128] = m;
+            park_i[192] = g.key; park_i[256] = g.k; park_i[320] = res.segments;
+        }
         const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, res.work, stk);
+        if constexpr (PARK) {
+            // the walk's stack stores may alias these slots as far as the compiler can tell: the
+            // values are reloaded, not forwarded, so their registers are free during the walk
+            T = mk<R>((R)park_d[0], (R)park_d[64], (R)park_d[128]);
+            depth = (int)park_i[0]; isegs = park_i[64]; m = park_i[128];
+            g.key = park_i[192]; g.k = park_i[256]; res.segments = park_i[320];
+            if (COUNT) q = (size_t)(tl.y0 + (int)(m / (uint32_t)vw)) * im.cw + (tl.x0 + (int)(m % (uint32_t)vw));
+        }
         const uint64_t t1 = RT_TICK();
         if (RT_PROFILE) res.cyc[0] += t1 - t0;
         ++res.segments;
@@ -245,11 +279,13 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
 }
 
 // sum[q] += part[c][tile][.][m] for c = 0 .. chunks-1 in chunk order (binary64); one thread per pixel,
-// a wave per tile (its reads of one chunk are 3 x 512 contiguous bytes)
-__global__ __launch_bounds__(256) void reduce_kernel(const ImageParams im, double* __restrict__ sum,
-                                                     const double* __restrict__ part, const int tiles,
-                                                     const int chunks) {
-    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6), m = threadIdx.x & 63;
+// one one-wave workgroup per tile (its reads of one chunk are 3 x 512 contiguous bytes).  One-wave
+// workgroups: while the next batch's trace waves hold the CUs (overlapped batches), a 256-thread
+// workgroup waits for four free wave slots on one CU and was measured to take 7.8 ms instead of 0.1.
+__global__ __launch_bounds__(64) void reduce_kernel(const ImageParams im, double* __restrict__ sum,
+                                                    const double* __restrict__ part, const int tiles,
+                                                    const int chunks) {
+    const int tile = blockIdx.x, m = threadIdx.x;
     if (tile >= tiles) return;
     const Tile t = tile_of(im, tile);
     if (m >= t.nv) return;
@@ -302,6 +338,13 @@ template <int ACC, class R>
 static size_t stack_lds_bytes(const SceneView<R>& sc) {
     return ACC >= ACC_BVH_STACK && sizeof(R) == 4 ? (size_t)std::min(sc.stack_entries, RT_BVH_STACK) * 64 * sizeof(int) : 0;
 }
+// ... of the pool kernel (RT_PARK: the parked path state + the stack, binary64)
+template <int ACC, class R>
+static size_t pool_lds_bytes(const SceneView<R>& sc) {
+    if constexpr (parks<R, ACC>())
+        return (size_t)64 * (kParkDoubles * sizeof(double) + kParkInts * 4 + std::min(sc.stack_entries, RT_BVH_STACK) * 4);
+    return stack_lds_bytes<ACC>(sc);
+}
 
 static int crop_tiles(int cw, int ch) { return ((cw + 7) / 8) * ((ch + 7) / 8); }
 
@@ -315,7 +358,7 @@ size_t pool_partial_bytes(int cw, int ch, int ns, bool tri_bvh, int chunk_overri
 template <class R, int ACC>
 static void launch_pool_kernel(const TraceArgs<R>& a, bool count, double* part, int tiles, int chunks, int chunk,
                                hipStream_t stream) {
-    const size_t lds = stack_lds_bytes<ACC>(a.sc);
+    const size_t lds = pool_lds_bytes<ACC>(a.sc);
     if (count) hipLaunchKernelGGL((trace_pool_kernel<R, true, ACC>), dim3(tiles * chunks), dim3(64), lds, stream, a, part, tiles, chunk);
     else hipLaunchKernelGGL((trace_pool_kernel<R, false, ACC>), dim3(tiles * chunks), dim3(64), lds, stream, a, part, tiles, chunk);
 }
@@ -346,7 +389,7 @@ static hipError_t launch_pool(const TraceArgs<R>& a0, bool count, hipStream_t st
         double* part = chunks > 1 ? a0.c.part : nullptr;
         launch_pool_kernel<R, ACC>(a, count, part, tiles, chunks, chunk, stream);
         if (part)
-            hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, stream, a.im, a.c.sum,
+            hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)tiles), dim3(64), 0, stream, a.im, a.c.sum,
                                (const double*)part, tiles, chunks);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -429,8 +472,7 @@ template hipError_t launch_trace_partials<float>(const SceneView<float>&, const 
 hipError_t launch_reduce(const ImageParams& im, double* sum, const double* part, bool tri_bvh, hipStream_t stream) {
     if (im.cw <= 0 || im.ch <= 0 || im.s_end <= im.s_begin) return hipSuccess;
     const PoolPlan p = pool_plan(im.cw, im.ch, im.s_end - im.s_begin, tri_bvh, im.pool_chunk);
-    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((p.tiles + 3) / 4)), dim3(256), 0, stream, im, sum, part, p.tiles,
-                       p.chunks);
+    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)p.tiles), dim3(64), 0, stream, im, sum, part, p.tiles, p.chunks);
     return hipGetLastError();
 }
 
@@ -488,7 +530,8 @@ __device__ __forceinline__ uint8_t to_u8(double c) {
     return v != v ? (uint8_t)0 : (uint8_t)v;                  // Uint8ClampedArray stores NaN as 0
 }
 
-__global__ __launch_bounds__(256) void finalize_kernel(const FinalizeParams p, const double* __restrict__ sum,
+// one-wave workgroups, like reduce_kernel: the preview frames run beside trace waves
+__global__ __launch_bounds__(64) void finalize_kernel(const FinalizeParams p, const double* __restrict__ sum,
                                                        double* __restrict__ mean, float* __restrict__ post,
                                                        uint8_t* __restrict__ rgba8) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -514,7 +557,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(const FinalizeParams p, c
 hipError_t launch_finalize(const FinalizeParams& p, const double* sum, double* mean, float* post, uint8_t* rgba8,
                            hipStream_t stream) {
     if (p.n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(finalize_kernel, dim3((p.n + 255) / 256), dim3(256), 0, stream, p, sum, mean, post, rgba8);
+    hipLaunchKernelGGL(finalize_kernel, dim3((p.n + 63) / 64), dim3(64), 0, stream, p, sum, mean, post, rgba8);
     return hipGetLastError();
 }
 

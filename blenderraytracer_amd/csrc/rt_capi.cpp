@@ -141,6 +141,10 @@ double now_ms() {
     return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
 }
 
+// Batches in flight per render (render_impl): partial slots, trace streams, preview staging.  The
+// host queues up to kSlots - 1 batches ahead of the one it waits for.
+constexpr int kSlots = 3;
+
 // Everything one device holds for a scene: the scene arrays in its HBM, a stream, the running sums
 // and counters of the samples it traces, the pool's chunk partials and the work totals (scratch).
 struct DeviceState {
@@ -157,11 +161,13 @@ struct DeviceState {
     hipStream_t scratch_stream = nullptr;
     bool scratch_used = false;
     hipEvent_t copy_ev = nullptr;      // a replica's batch sums copied out to the home device (merge_shards)
-    // overlapped batches (render_impl): batch k traces on tstream[k % 2] into its own partials, so the
-    // next batch's waves fill the CUs while this one drains; its reduce runs on `stream` in batch order
-    hipStream_t tstream[2] = {};
-    DevBuf<double> part2;              // partials of slot 1
-    hipEvent_t traced[2] = {}, reduced[2] = {}, setup_ev = nullptr;
+    // overlapped batches (render_impl): batch k traces on tstream[k % kSlots] into its own partials
+    // (slot 0: `part`), so the next batches' waves fill the CUs while this one drains; its reduce runs on
+    // `stream` in batch order
+    hipStream_t tstream[kSlots] = {};
+    DevBuf<double> part_more[kSlots - 1];   // partials of slots 1 ..
+    hipEvent_t traced[kSlots] = {}, reduced[kSlots] = {}, setup_ev = nullptr;
+    DevBuf<double>& slot_part(int j) { return j == 0 ? part : part_more[j - 1]; }
 
     int init(int dev, const HostScene& hs, const rt_scene_desc& d) {
         device = dev;
@@ -169,11 +175,16 @@ struct DeviceState {
         if (e != hipSuccess) return fail(RT_ERR_DEVICE, "hipSetDevice(%d): %s", dev, hipGetErrorString(e));
         int rc;
         if ((rc = build_device(s64, hs, d)) || (rc = build_device(s32, hs, d))) return rc;
-        e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
-        for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipStreamCreateWithFlags(&tstream[k], hipStreamNonBlocking);
+        // the accumulation stream at the device's highest priority: a batch's reduce (and preview frame)
+        // would otherwise wait for free wave slots behind the next batch's trace waves — measured: a
+        // 0.1-ms reduce took 7.8 ms, and the batch after next started late
+        int least = 0, greatest = 0;
+        e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, greatest);
+        for (int k = 0; k < kSlots && e == hipSuccess; ++k) e = hipStreamCreateWithFlags(&tstream[k], hipStreamNonBlocking);
         for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreate(&ev[k]);
-        for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&traced[k], hipEventDisableTiming);
-        for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&reduced[k], hipEventDisableTiming);
+        for (int k = 0; k < kSlots && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&traced[k], hipEventDisableTiming);
+        for (int k = 0; k < kSlots && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&reduced[k], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&setup_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&scratch_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&copy_ev, hipEventDisableTiming);
@@ -182,18 +193,24 @@ struct DeviceState {
     }
     void sync_all() {                  // every stream of this device (error paths, release)
         (void)hipSetDevice(device);
-        for (hipStream_t s : {tstream[0], tstream[1], stream})
+        for (hipStream_t s : tstream)
             if (s) (void)hipStreamSynchronize(s);
+        if (stream) (void)hipStreamSynchronize(stream);
     }
     void release() {
         sync_all();
         s64.release();
         s32.release();
-        sum.release(); segs.release(); draws.release(); total.release(); part.release(); part2.release();
-        for (hipEvent_t e : {ev[0], ev[1], traced[0], traced[1], reduced[0], reduced[1], setup_ev, scratch_ev, copy_ev})
+        sum.release(); segs.release(); draws.release(); total.release(); part.release();
+        for (DevBuf<double>& b : part_more) b.release();
+        for (hipEvent_t e : {ev[0], ev[1], setup_ev, scratch_ev, copy_ev})
             if (e) (void)hipEventDestroy(e);
-        for (hipStream_t s : {tstream[0], tstream[1], stream})
-            if (s) (void)hipStreamDestroy(s);
+        for (int k = 0; k < kSlots; ++k) {
+            if (traced[k]) (void)hipEventDestroy(traced[k]);
+            if (reduced[k]) (void)hipEventDestroy(reduced[k]);
+            if (tstream[k]) (void)hipStreamDestroy(tstream[k]);
+        }
+        if (stream) (void)hipStreamDestroy(stream);
     }
 };
 
@@ -240,9 +257,9 @@ struct rt_scene {
     DevBuf<float> post, post_raw;   // post_raw: pre-denoise floatData
     DevBuf<uint8_t> rgba;
     DevBuf<uint8_t> preview;        // rt_output.preview_rgba8: the running frame of the last batch (device) ...
-    uint8_t* preview_host[2] = {};  // ... copied into pinned staging (one per in-flight batch)
+    uint8_t* preview_host[kSlots] = {};   // ... copied into pinned staging (one per in-flight batch)
     size_t preview_host_n = 0;
-    hipEvent_t batch_done[2] = {};  // home stream: batch k's reduce, merges and preview done (slot k % 2)
+    hipEvent_t batch_done[kSlots] = {};   // home stream: batch k's reduce, merges and preview done (slot k % kSlots)
     std::atomic<int> cancel{0};
     size_t ckpt_pixels = 0;         // progressive state of the last rt_render / rt_render_resume:
     int ckpt_done = 0;              // `home.sum` holds samples [sample_begin, ckpt_done) of ckpt_pixels pixels
@@ -335,7 +352,7 @@ hipError_t trace_overlapped(const rt_scene* sc, DeviceState& ds, const rt_settin
                             const Counters& c, int j, bool slot_used) {
     if (im.max_depth <= 0 || im.s_end <= im.s_begin) return hipSuccess;
     const bool bvh = use_bvh(sc, s);
-    DevBuf<double>& part = j == 0 ? ds.part : ds.part2;
+    DevBuf<double>& part = ds.slot_part(j);
     hipStream_t ts = ds.tstream[j];
     hipError_t e = hipSuccess;
     if (slot_used) e = hipStreamWaitEvent(ts, ds.reduced[j], 0);
@@ -414,17 +431,22 @@ int ensure_partials(const rt_scene* sc, DeviceState& ds, int cw, int ch, int sam
 // Both partial slots of the overlapped batches, `bytes` each (one batch's chunks: pool_plan).  False
 // (no error) when they do not fit the budget: the render then runs its batches one after the other.
 bool ensure_overlap_partials(DeviceState& ds, size_t bytes) {
-    const size_t have = std::min(ds.part.n, ds.part2.n) * sizeof(double);
-    if (bytes == 0 || (ds.part.p && ds.part2.p && have >= bytes)) return true;
+    bool have = true;
+    size_t held = 0;
+    for (int j = 0; j < kSlots; ++j) {
+        have = have && ds.slot_part(j).p && ds.slot_part(j).n * sizeof(double) >= bytes;
+        held += ds.slot_part(j).n * sizeof(double);
+    }
+    if (bytes == 0 || have) return true;
     if (scratch_idle(ds) != hipSuccess) return false;
     size_t free_b = 0, total_b = 0, cap = part_budget();
-    const size_t held = (ds.part.n + ds.part2.n) * sizeof(double);
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = std::min(cap, (free_b + held) / 10);
-    if (2 * bytes > cap) return false;
-    if (ds.part.ensure(bytes / sizeof(double)) != hipSuccess || ds.part2.ensure(bytes / sizeof(double)) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
+    if (kSlots * bytes > cap) return false;
+    for (int j = 0; j < kSlots; ++j)
+        if (ds.slot_part(j).ensure(bytes / sizeof(double)) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
     return true;
 }
 
@@ -581,7 +603,9 @@ void rt_scene_destroy(rt_scene* sc) {
     sc->preview.release();
     for (uint8_t* p : sc->preview_host)
         if (p) (void)hipHostFree(p);
-    for (hipEvent_t e : {sc->ev[0], sc->ev[1], sc->batch_done[0], sc->batch_done[1]})
+    for (hipEvent_t e : {sc->ev[0], sc->ev[1]})
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : sc->batch_done)
         if (e) (void)hipEventDestroy(e);
     delete sc;
 }
@@ -690,7 +714,8 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     auto batch_chunk = [&](int k, int ns) { return chunk_hint[k] > 0 ? std::max(1, std::min(chunk_hint[k], ns)) : 0; };
     // overlapped batches: the pool with several batches.  Not with per-pixel counters over several
     // devices: the trace kernels add those directly, and a replica's merge zeroes them between batches
-    bool overlap = pool && nb > 1 && s->max_depth > 0 && !(nsh > 1 && (want_segs || want_draws));
+    static const bool overlap_env = !(getenv("RT_OVERLAP") && getenv("RT_OVERLAP")[0] == '0');   // A/B runs
+    bool overlap = overlap_env && pool && nb > 1 && s->max_depth > 0 && !(nsh > 1 && (want_segs || want_draws));
     for (int k = 0; k < nsh; ++k) {
         DeviceState& ds = *states[k];
         HIP_TRY(hipSetDevice(ds.device));
@@ -765,7 +790,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     sc->ckpt_done = s0;
 
     // enqueue batch kb (no host wait): every shard's trace, the merge of the shards into the home device,
-    // the preview frame, then batch_done[kb % 2] on the home stream
+    // the preview frame, then batch_done[kb % kSlots] on the home stream
     auto enqueue = [&](int kb) -> int {
         const int b = s0 + kb * batch, be = std::min(s1, b + batch);
         for (int k = 0; k < nsh; ++k) {           // every shard's launches first: the devices run together
@@ -774,7 +799,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
             shard_range(b, be, k, nsh, bi.s_begin, bi.s_end);
             bi.pool_chunk = batch_chunk(k, bi.s_end - bi.s_begin);
             HIP_TRY(hipSetDevice(ds.device));
-            if (overlap) HIP_TRY(trace_overlapped(sc, ds, s, bi, cs[k], kb % 2, kb >= 2));
+            if (overlap) HIP_TRY(trace_overlapped(sc, ds, s, bi, cs[k], kb % kSlots, kb >= kSlots));
             else HIP_TRY(trace(sc, ds, s, bi, cs[k], ds.stream));
         }
         int r;
@@ -783,36 +808,40 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         if (want_preview && be < s1) {            // the running frame: mean over the samples so far
             FinalizeParams fp{(int)n, be - base, s->tone_map, s->exposure, s->gamma};
             HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview.p, h.stream));
-            HIP_TRY(hipMemcpyAsync(sc->preview_host[kb % 2], sc->preview.p, 4 * n, hipMemcpyDeviceToHost, h.stream));
+            HIP_TRY(hipMemcpyAsync(sc->preview_host[kb % kSlots], sc->preview.p, 4 * n, hipMemcpyDeviceToHost, h.stream));
         }
-        HIP_TRY(hipEventRecord(sc->batch_done[kb % 2], h.stream));
+        HIP_TRY(hipEventRecord(sc->batch_done[kb % kSlots], h.stream));
         return RT_OK;
     };
     // host side of batch kb once batch_done: checkpoint state and the preview frame
     auto complete = [&](int kb) -> int {
-        HIP_TRY(hipEventSynchronize(sc->batch_done[kb % 2]));
+        HIP_TRY(hipEventSynchronize(sc->batch_done[kb % kSlots]));
         const int be = std::min(s1, s0 + (kb + 1) * batch);
         sc->ckpt_done = be;
-        if (want_preview && be < s1) memcpy(out->preview_rgba8, sc->preview_host[kb % 2], 4 * n);
+        if (want_preview && be < s1) memcpy(out->preview_rgba8, sc->preview_host[kb % kSlots], 4 * n);
         return RT_OK;
     };
+    // the host keeps up to kSlots - 1 batches queued beyond the one it waits for: a batch's reduce waits
+    // behind the next batch's trace waves for free wave slots, so the batch after next must not depend on
+    // the host seeing this one complete
     int status = RT_OK, enqueued = 0;
-    if (nb > 0) {
-        status = enqueue(0);
-        enqueued = status == RT_OK ? 1 : 0;
-    }
-    for (int kb = 0; kb < nb && status == RT_OK; ++kb) {
-        if (enqueued == kb + 1 && kb + 1 < nb && !sc->cancel.load()) {
-            if ((status = enqueue(kb + 1))) break;
-            enqueued = kb + 2;
+    auto fill = [&](int upto) -> int {          // enqueue batches [enqueued, upto)
+        for (; enqueued < std::min(upto, nb) && !sc->cancel.load(); ++enqueued) {
+            const int r = enqueue(enqueued);
+            if (r) return r;
         }
+        return RT_OK;
+    };
+    for (int kb = 0; kb < nb && status == RT_OK; ++kb) {
+        if ((status = fill(kb + kSlots))) break;
         if ((status = complete(kb))) break;
         const int be = sc->ckpt_done;
         if (progress && be < s1 && progress((double)(be - s0) / (double)(s1 - s0), user)) sc->cancel.store(1);
         if (sc->cancel.load()) {
-            if (enqueued > kb + 1 && (status = complete(kb + 1))) break;   // the batch in flight finishes
-            // ... and if it was the last one, the render has completed
-            if (sc->ckpt_done < s1) status = fail(RT_ERR_CANCELLED, "render cancelled after %d samples", sc->ckpt_done);
+            // the batches in flight finish (and if the last one was among them, the render completed)
+            for (int k = kb + 1; k < enqueued && status == RT_OK; ++k) status = complete(k);
+            if (status == RT_OK && sc->ckpt_done < s1)
+                status = fail(RT_ERR_CANCELLED, "render cancelled after %d samples", sc->ckpt_done);
             break;
         }
     }

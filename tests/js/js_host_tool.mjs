@@ -70,10 +70,10 @@ if (cmd === 'pack') {
     // progressive: window.renderCancelled mid-frame, then resume() from the checkpoint
     {
         const { rt: full } = tracerFor('kitchen_sink', { batchSamples: 2 });   // same sample batches
-        full.updateRenderSettings({ samples: 8 });
+        full.updateRenderSettings({ samples: 16 });
         await full.render();
         const { rt: part } = tracerFor('kitchen_sink', { batchSamples: 2 });
-        part.updateRenderSettings({ samples: 8 });
+        part.updateRenderSettings({ samples: 16 });
         global.window = { renderCancelled: false };
         let calls = 0;
         await part.render(() => { if (++calls === 2) global.window.renderCancelled = true; });
