@@ -256,8 +256,9 @@ struct rt_scene {
     std::vector<MergeSlot> merge;   // per shard (index in the render's device list): its staging on home
     DevBuf<float> post, post_raw;   // post_raw: pre-denoise floatData
     DevBuf<uint8_t> rgba;
-    DevBuf<uint8_t> preview;        // rt_output.preview_rgba8: the running frame of the last batch (device) ...
-    uint8_t* preview_host[kSlots] = {};   // ... copied into pinned staging (one per in-flight batch)
+    // rt_output.preview_rgba8: the running frame of each batch in flight, in mapped pinned host memory
+    uint8_t* preview_host[kSlots] = {};
+    uint8_t* preview_dev[kSlots] = {};    // the same buffers' device addresses
     size_t preview_host_n = 0;
     hipEvent_t batch_done[kSlots] = {};   // home stream: batch k's reduce, merges and preview done (slot k % kSlots)
     std::atomic<int> cancel{0};
@@ -600,7 +601,6 @@ void rt_scene_destroy(rt_scene* sc) {
         if (m.added) (void)hipEventDestroy(m.added);
     }
     sc->rgba.release();
-    sc->preview.release();
     for (uint8_t* p : sc->preview_host)
         if (p) (void)hipHostFree(p);
     for (hipEvent_t e : {sc->ev[0], sc->ev[1]})
@@ -775,14 +775,16 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     for (hipEvent_t& e : sc->batch_done)
         if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (want_preview) {
-        HIP_TRY(sc->preview.ensure(4 * n));
         if (sc->preview_host_n < 4 * n) {
             for (uint8_t*& p : sc->preview_host) {
                 if (p) (void)hipHostFree(p);
                 p = nullptr;
             }
             sc->preview_host_n = 0;
-            for (uint8_t*& p : sc->preview_host) HIP_TRY(hipHostMalloc((void**)&p, 4 * n, hipHostMallocDefault));
+            for (int k = 0; k < kSlots; ++k) {
+                HIP_TRY(hipHostMalloc((void**)&sc->preview_host[k], 4 * n, hipHostMallocMapped));
+                HIP_TRY(hipHostGetDevicePointer((void**)&sc->preview_dev[k], sc->preview_host[k], 0));
+            }
             sc->preview_host_n = 4 * n;
         }
     }
@@ -806,9 +808,11 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         if (nsh > 1 && (r = merge_shards(sc, states, n, want_segs, want_draws))) return r;
         HIP_TRY(hipSetDevice(h.device));
         if (want_preview && be < s1) {            // the running frame: mean over the samples so far
+            // written by the epilogue kernel straight into pinned host memory (over PCIe): a
+            // hipMemcpyAsync here is a blit kernel that waits for wave slots behind the trace waves
+            // (measured 7-15 ms per 8-MB frame while batches overlap)
             FinalizeParams fp{(int)n, be - base, s->tone_map, s->exposure, s->gamma};
-            HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview.p, h.stream));
-            HIP_TRY(hipMemcpyAsync(sc->preview_host[kb % kSlots], sc->preview.p, 4 * n, hipMemcpyDeviceToHost, h.stream));
+            HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview_dev[kb % kSlots], h.stream));
         }
         HIP_TRY(hipEventRecord(sc->batch_done[kb % kSlots], h.stream));
         return RT_OK;
