@@ -239,13 +239,16 @@ def node_end_to_end(cfg, args):
     finally:
         os.unlink(path)
     return {"value": round(out["value"], 3), "unit": "Msamples/s", "wall_ms": round(out["wall_ms"], 3),
-            "first_call_ms": round(out["first_call_ms"], 3), "kernel_ms": out["kernel_ms"],
-            "progress_calls": out.get("progress_calls"), "one_batch_wall_ms": out.get("one_batch_wall_ms"),
+            "walls_ms": [round(w, 3) for w in out["walls_ms"]], "reps": out["reps"],
+            "first_call_ms": round(out["first_call_ms"], 3), "kernel_ms": round(out["kernel_ms"], 3),
+            "rt_render_wall_ms": round(out["rt_render_wall_ms"], 3),
+            "progress_calls": out["progress_calls"], "no_preview_wall_ms": round(out["no_preview_wall_ms"], 3),
+            "one_batch_wall_ms": round(out["one_batch_wall_ms"], 3), "one_batch_kernel_ms": round(out["one_batch_kernel_ms"], 3),
             "what": "GpuRayTracer.render() from Node (the installGpuRender path): scene resident from the first call "
                     "(first_call_ms includes its upload and BVH build), pack + compare, trace in 16 progressive "
                     "sample batches (onProgress + the running frame in imageData after each), epilogue, RGBA8 "
-                    "into imageData (what the reference's render() produces); one_batch_wall_ms: the same frame "
-                    "as one batch"}
+                    "into imageData (what the reference's render() produces); median of `reps` after a warm-up; "
+                    "no_preview / one_batch: the same frame without preview frames / as one sample batch"}
 
 
 def build_provenance():

@@ -64,7 +64,7 @@ class Settings(C.Structure):
 class Output(C.Structure):
     _fields_ = [("mean", C.POINTER(C.c_double)), ("post", C.POINTER(C.c_float)), ("rgba8", C.POINTER(C.c_uint8)),
                 ("segments", C.POINTER(C.c_uint32)), ("draws", C.POINTER(C.c_uint32)),
-                ("preview_rgba8", C.POINTER(C.c_uint8))]
+                ("preview_rgba8", C.POINTER(C.c_uint8)), ("preview_samples", C.POINTER(C.c_int32))]
 
 
 class Stats(C.Structure):

@@ -18,7 +18,9 @@
 #include <node_api.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <mutex>
 #include <cstring>
@@ -210,6 +212,8 @@ struct RenderJob {
     void* out_ptr[OUT_N] = {};
     napi_ref caller_rgba = nullptr;  // settings.outRgba8
     std::vector<uint8_t> preview;    // rt_output.preview_rgba8 (settings.preview)
+    int32_t preview_samples = 0;     // rt_output.preview_samples: the frame's samples (written by the worker)
+    int32_t shown_samples = -1;      // the frame last copied into the caller's imageData (main thread)
     // progress hand-off: the worker waits until the main thread ran the JS callback
     std::mutex m;
     std::condition_variable cv;
@@ -236,9 +240,11 @@ uint8_t* live_bytes(napi_env env, napi_ref ref, size_t bytes) {
 void call_progress(napi_env env, napi_value js_cb, void*, void* data) {
     RenderJob* job = static_cast<RenderJob*>(data);     // alive: the worker waits for this call
     if (env) {
-        if (!job->preview.empty())
-            if (uint8_t* dst = live_bytes(env, job->caller_rgba, job->preview.size()))
+        if (!job->preview.empty() && job->preview_samples != job->shown_samples)   // a newer frame only
+            if (uint8_t* dst = live_bytes(env, job->caller_rgba, job->preview.size())) {
                 std::memcpy(dst, job->preview.data(), job->preview.size());
+                job->shown_samples = job->preview_samples;
+            }
         if (js_cb) {
             napi_value arg, undef;
             napi_create_double(env, job->fraction, &arg);
@@ -251,8 +257,16 @@ void call_progress(napi_env env, napi_value js_cb, void*, void* data) {
     job->cv.notify_all();
 }
 
+// RT_NAPI_TRACE=1 (developer A/B): stderr timestamps of the progress hand-off
+double trace_ms() {
+    static const bool on = getenv("RT_NAPI_TRACE") && getenv("RT_NAPI_TRACE")[0] == '1';
+    if (!on) return -1;
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int progress_hook(double fraction, void* user) {
     RenderJob* job = static_cast<RenderJob*>(user);
+    const double t0 = trace_ms();
     if (job->tsfn) {
         {
             std::lock_guard<std::mutex> lk(job->m);
@@ -264,6 +278,7 @@ int progress_hook(double fraction, void* user) {
             job->cv.wait(lk, [job] { return !job->pending; });
         }
     }
+    if (t0 >= 0) fprintf(stderr, "[napi] progress %.3f at %.3f ms, hand-off %.3f ms\n", fraction, t0, trace_ms() - t0);
     return job->cancel_from_js.load();
 }
 
@@ -276,12 +291,16 @@ void execute(napi_env, void* data) {
     out.segments = static_cast<uint32_t*>(job->out_ptr[RenderJob::OUT_SEGS]);
     out.draws = static_cast<uint32_t*>(job->out_ptr[RenderJob::OUT_DRAWS]);
     out.preview_rgba8 = job->preview.empty() ? nullptr : job->preview.data();
+    out.preview_samples = &job->preview_samples;
+    const double t0 = trace_ms();
+    if (t0 >= 0) fprintf(stderr, "[napi] rt_render start %.3f ms\n", t0);
     if (job->resume_done >= 0)
         job->status = rt_render_resume(job->scene, &job->st, job->resume.data(), job->resume_done, &out, progress_hook,
                                        job, &job->stats);
     else
         job->status = rt_render(job->scene, &job->st, &out, progress_hook, job, &job->stats);
     if (job->status != RT_OK) job->error = rt_last_error();
+    if (t0 >= 0) fprintf(stderr, "[napi] rt_render end %.3f ms (%.3f)\n", trace_ms(), trace_ms() - t0);
 }
 
 // A new ArrayBuffer of `bytes` on the main thread, referenced by the job until it completes.

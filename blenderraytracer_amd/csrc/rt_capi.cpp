@@ -141,9 +141,11 @@ double now_ms() {
     return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
 }
 
-// Batches in flight per render (render_impl): partial slots, trace streams, preview staging.  The
-// host queues up to kSlots - 1 batches ahead of the one it waits for.
+// Batches in flight per render (render_impl): kSlots partial slots / trace streams; the host queues up
+// to kSlots batches beyond the one it waits for, each with its own preview staging and completion event
+// (kDone of them, so a queued batch never writes a frame the host has not read yet).
 constexpr int kSlots = 3;
+constexpr int kDone = 2 * kSlots;
 
 // Everything one device holds for a scene: the scene arrays in its HBM, a stream, the running sums
 // and counters of the samples it traces, the pool's chunk partials and the work totals (scratch).
@@ -257,10 +259,10 @@ struct rt_scene {
     DevBuf<float> post, post_raw;   // post_raw: pre-denoise floatData
     DevBuf<uint8_t> rgba;
     // rt_output.preview_rgba8: the running frame of each batch in flight, in mapped pinned host memory
-    uint8_t* preview_host[kSlots] = {};
-    uint8_t* preview_dev[kSlots] = {};    // the same buffers' device addresses
+    uint8_t* preview_host[kDone] = {};
+    uint8_t* preview_dev[kDone] = {};     // the same buffers' device addresses
     size_t preview_host_n = 0;
-    hipEvent_t batch_done[kSlots] = {};   // home stream: batch k's reduce, merges and preview done (slot k % kSlots)
+    hipEvent_t batch_done[kDone] = {};    // home stream: batch k's reduce, merges and preview done (slot k % kDone)
     std::atomic<int> cancel{0};
     size_t ckpt_pixels = 0;         // progressive state of the last rt_render / rt_render_resume:
     int ckpt_done = 0;              // `home.sum` holds samples [sample_begin, ckpt_done) of ckpt_pixels pixels
@@ -781,7 +783,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
                 p = nullptr;
             }
             sc->preview_host_n = 0;
-            for (int k = 0; k < kSlots; ++k) {
+            for (int k = 0; k < kDone; ++k) {
                 HIP_TRY(hipHostMalloc((void**)&sc->preview_host[k], 4 * n, hipHostMallocMapped));
                 HIP_TRY(hipHostGetDevicePointer((void**)&sc->preview_dev[k], sc->preview_host[k], 0));
             }
@@ -791,8 +793,9 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     sc->ckpt_pixels = n;
     sc->ckpt_done = s0;
 
+    int enqueued = 0;                             // batches [0, enqueued) are queued on the GPU
     // enqueue batch kb (no host wait): every shard's trace, the merge of the shards into the home device,
-    // the preview frame, then batch_done[kb % kSlots] on the home stream
+    // the preview frame, then batch_done[kb % kDone] on the home stream
     auto enqueue = [&](int kb) -> int {
         const int b = s0 + kb * batch, be = std::min(s1, b + batch);
         for (int k = 0; k < nsh; ++k) {           // every shard's launches first: the devices run together
@@ -812,23 +815,29 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
             // hipMemcpyAsync here is a blit kernel that waits for wave slots behind the trace waves
             // (measured 7-15 ms per 8-MB frame while batches overlap)
             FinalizeParams fp{(int)n, be - base, s->tone_map, s->exposure, s->gamma};
-            HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview_dev[kb % kSlots], h.stream));
+            HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview_dev[kb % kDone], h.stream));
         }
-        HIP_TRY(hipEventRecord(sc->batch_done[kb % kSlots], h.stream));
+        HIP_TRY(hipEventRecord(sc->batch_done[kb % kDone], h.stream));
         return RT_OK;
     };
     // host side of batch kb once batch_done: checkpoint state and the preview frame
     auto complete = [&](int kb) -> int {
-        HIP_TRY(hipEventSynchronize(sc->batch_done[kb % kSlots]));
+        HIP_TRY(hipEventSynchronize(sc->batch_done[kb % kDone]));
         const int be = std::min(s1, s0 + (kb + 1) * batch);
         sc->ckpt_done = be;
-        if (want_preview && be < s1) memcpy(out->preview_rgba8, sc->preview_host[kb % kSlots], 4 * n);
+        // the running frame, unless the next batch has finished too (its frame supersedes this one: the
+        // host does not fall further behind the GPU copying frames nobody will see)
+        if (want_preview && be < s1 &&
+            !(kb + 1 < enqueued && hipEventQuery(sc->batch_done[(kb + 1) % kDone]) == hipSuccess)) {
+            memcpy(out->preview_rgba8, sc->preview_host[kb % kDone], 4 * n);
+            if (out->preview_samples) *out->preview_samples = be - base;
+        }
         return RT_OK;
     };
-    // the host keeps up to kSlots - 1 batches queued beyond the one it waits for: a batch's reduce waits
-    // behind the next batch's trace waves for free wave slots, so the batch after next must not depend on
-    // the host seeing this one complete
-    int status = RT_OK, enqueued = 0;
+    // the host keeps up to kSlots batches queued beyond the one it waits for (their ordering on the
+    // partial slots is device-side: trace_overlapped), so neither the host's progress call nor a preview
+    // frame ever delays the start of a batch
+    int status = RT_OK;
     auto fill = [&](int upto) -> int {          // enqueue batches [enqueued, upto)
         for (; enqueued < std::min(upto, nb) && !sc->cancel.load(); ++enqueued) {
             const int r = enqueue(enqueued);
@@ -837,7 +846,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         return RT_OK;
     };
     for (int kb = 0; kb < nb && status == RT_OK; ++kb) {
-        if ((status = fill(kb + kSlots))) break;
+        if ((status = fill(kb + kSlots + 1))) break;
         if ((status = complete(kb))) break;
         const int be = sc->ckpt_done;
         if (progress && be < s1 && progress((double)(be - s0) / (double)(s1 - s0), user)) sc->cancel.store(1);

@@ -185,7 +185,11 @@ typedef struct rt_output {
                                  the RGBA8 frame of the samples traced so far (mean over those samples, tone
                                  map, gamma; no denoise, like the reference's rows before its final pass).
                                  A cancel is observed after a batch, the batch already in flight completes,
-                                 and the buffer then holds the frame of the checkpointed samples */
+                                 and the buffer then holds the frame of the checkpointed samples.  A batch
+                                 whose successor has already finished when the host gets to it is skipped
+                                 (the buffer keeps the previous frame until the newer one is copied) */
+    int32_t* preview_samples; /* optional out: the samples (from sample_begin) in preview_rgba8's frame,
+                                 updated with it */
 } rt_output;
 
 typedef struct rt_stats {

@@ -18,5 +18,5 @@ for f in glob.glob(os.path.join(d, "**", "*memory_copy_trace.csv"), recursive=Tr
 rows.sort()
 rows = [r for r in rows if flt in r[2]] if flt else rows
 t0 = rows[0][0]
-for s, e, n, q in rows[-80:]:
+for s, e, n, q in (rows if os.environ.get("TL_ALL") else rows[-80:]):
     print(f"{(s - t0) / 1e6:10.3f} {(e - t0) / 1e6:10.3f} {(e - s) / 1e6:8.3f} ms  q{q:>3} {n}")

@@ -149,9 +149,10 @@ def test_deterministic_and_progress(gpu):
 
 
 def test_cancel_via_progress(gpu):
-    rt = _rtow(64, 36, 8)
+    rt = _rtow(64, 36, 16)
     with pytest.raises(RuntimeError, match="CANCELLED"):
-        rt.render(batch_samples=2, on_progress=lambda f: True)
+        rt.render(batch_samples=1, on_progress=lambda f: True)
+    assert rt.checkpoint()[1] == 4            # the first batch and the three queued behind it
 
 
 def test_max_depth_zero_is_black(gpu):
@@ -245,7 +246,7 @@ def test_checkpoint_resume_is_bit_exact(gpu):
     with pytest.raises(RuntimeError, match="CANCELLED"):
         rt.render(batch_samples=1, on_progress=lambda f: calls.append(f) or len(calls) >= 2)
     sums, done = rt.checkpoint()
-    assert done == 4 and sums.shape == (54, 96, 3)     # cancelled after batch 2: batches 3 and 4 were in flight
+    assert done == 5 and sums.shape == (54, 96, 3)     # cancelled after batch 2: batches 3 to 5 were in flight
     rt.close()
     rt2 = _rtow(96, 54, 10)
     res = rt2.render(want=("mean",), resume=(sums, done), batch_samples=1)
@@ -420,7 +421,7 @@ def test_multi_device_checkpoint_resume(gpu):
     with pytest.raises(RuntimeError, match="CANCELLED"):
         rt.render(batch_samples=2, devices=[0, 0], on_progress=lambda f: calls.append(f) or len(calls) >= 1)
     sums, done = rt.checkpoint()
-    assert done == 6
+    assert done == 8                                   # cancelled after batch 1: batches 2 to 4 were in flight
     rt.close()
     rt2 = _rtow(96, 54, 10)
     res = rt2.render(want=("mean",), resume=(sums, done), batch_samples=2, devices=[0, 0])
@@ -630,7 +631,7 @@ def test_progressive_preview_and_cancel(gpu):
     with pytest.raises(RuntimeError, match="CANCELLED"):
         rt.render(want=("preview",), batch_samples=2, on_progress=lambda f: calls.append(f) or len(calls) >= 5)
     sums, done = rt.checkpoint()
-    assert done == 14                                            # 5 batches + the two in flight
+    assert done == 16                                            # 5 batches + the three in flight
     cancelled = rt.image_data.copy()
     rt2 = _rtow(128, 72, done, seed=6)                           # exactly the checkpointed samples
     ref = rt2.render(batch_samples=2)
