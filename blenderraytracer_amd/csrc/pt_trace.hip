@@ -39,8 +39,16 @@ struct TraceArgs {
 #define RT_BVH_WAVES_F32 5        // binary32 BVH walk: 96 VGPRs (measured 4/5/6 waves: 6070/6628/6542)
 #endif
 
+#ifndef RT_SPHERES_WAVES_PER_SIMD
+#define RT_SPHERES_WAVES_PER_SIMD 5   // binary64 sphere-only walk (ACC_BVH_SPHERES): 96 VGPRs (4 / 5 waves: 7157 / 7407)
+#endif
+#ifndef RT_SPHERES_WAVES_F32
+#define RT_SPHERES_WAVES_F32 6       // binary32 sphere-only walk: 80 VGPRs (5 / 6 waves: 8536 / 8800 RTOW f32)
+#endif
+
 template <class R, int ACC>
 constexpr int waves_per_simd() {
+    if constexpr (ACC == ACC_BVH_SPHERES) return sizeof(R) == 8 ? RT_SPHERES_WAVES_PER_SIMD : RT_SPHERES_WAVES_F32;
     return ACC >= ACC_BVH ? (sizeof(R) == 8 ? RT_BVH_WAVES_PER_SIMD : RT_BVH_WAVES_F32) : RT_MIN_WAVES_PER_SIMD;
 }
 
@@ -397,14 +405,16 @@ static hipError_t launch_pool(const TraceArgs<R>& a0, bool count, hipStream_t st
     return hipSuccess;
 }
 
-// RT_BVH_WALK=skip (A/B runs): the stackless preorder walk; default: the ordered two-child walk
-static int bvh_walk_mode() {
+// RT_BVH_WALK=skip (A/B runs): the stackless preorder walk; default: the ordered two-child walk, in its
+// sphere-only form for scenes without triangles (RT_BVH_WALK=two: always the general form)
+template <class R>
+static int bvh_walk_mode(const SceneView<R>& sc) {
     static int v = -1;
     if (v == -1) {
         const char* e = getenv("RT_BVH_WALK");
-        v = e && !strncmp(e, "skip", 4) ? ACC_BVH : ACC_BVH_STACK;
+        v = e && !strncmp(e, "skip", 4) ? ACC_BVH : e && !strncmp(e, "two", 3) ? ACC_BVH_STACK : ACC_BVH_SPHERES;
     }
-    return v;
+    return v == ACC_BVH_SPHERES && sc.num_tri_nodes > 0 ? ACC_BVH_STACK : v;
 }
 
 template <class R, int ACC>
@@ -424,7 +434,9 @@ hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Cou
     TraceArgs<R> a{sc, im, c};
     const bool count = c.segs || c.draws;
     if (!bvh) return launch_acc<R, ACC_BRUTE>(a, count, pool, stream);
-    if (bvh_walk_mode() == ACC_BVH) return launch_acc<R, ACC_BVH>(a, count, pool, stream);
+    const int mode = bvh_walk_mode(sc);
+    if (mode == ACC_BVH) return launch_acc<R, ACC_BVH>(a, count, pool, stream);
+    if (mode == ACC_BVH_SPHERES) return launch_acc<R, ACC_BVH_SPHERES>(a, count, pool, stream);
     return launch_acc<R, ACC_BVH_STACK>(a, count, pool, stream);
 }
 
@@ -460,7 +472,9 @@ hipError_t launch_trace_partials(const SceneView<R>& sc, const ImageParams& im, 
     TraceArgs<R> a{sc, im, c};
     const bool count = c.segs || c.draws;
     if (!bvh) return launch_partials_acc<R, ACC_BRUTE>(a, count, p, part, stream);
-    if (bvh_walk_mode() == ACC_BVH) return launch_partials_acc<R, ACC_BVH>(a, count, p, part, stream);
+    const int mode = bvh_walk_mode(sc);
+    if (mode == ACC_BVH) return launch_partials_acc<R, ACC_BVH>(a, count, p, part, stream);
+    if (mode == ACC_BVH_SPHERES) return launch_partials_acc<R, ACC_BVH_SPHERES>(a, count, p, part, stream);
     return launch_partials_acc<R, ACC_BVH_STACK>(a, count, p, part, stream);
 }
 
@@ -499,7 +513,9 @@ hipError_t launch_closest_hits(const SceneView<R>& sc, bool bvh, const double* r
                                int* idx, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 63) / 64));
-    if (bvh) hipLaunchKernelGGL((closest_hits_kernel<R, ACC_BVH_STACK>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);
+    if (bvh && bvh_walk_mode(sc) == ACC_BVH_SPHERES)   // the walk the trace kernel runs on this scene
+        hipLaunchKernelGGL((closest_hits_kernel<R, ACC_BVH_SPHERES>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);
+    else if (bvh) hipLaunchKernelGGL((closest_hits_kernel<R, ACC_BVH_STACK>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);
     else hipLaunchKernelGGL((closest_hits_kernel<R, ACC_BRUTE>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);
     return hipGetLastError();
 }
