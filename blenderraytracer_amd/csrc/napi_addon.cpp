@@ -124,6 +124,9 @@ struct SceneBox {
     rt_scene* sc = nullptr;
     bool busy = false;
     size_t last_pixels = 0;         // crop pixels of the last render (checkpoint size)
+    // frame buffers of render() into a caller's imageData, reused from render to render (no per-frame
+    // allocation or page faults): the finished RGBA8 frame and the running preview frame
+    std::vector<uint8_t> frame, preview;
 };
 
 void scene_finalize(napi_env, void* data, void*) {
@@ -211,9 +214,10 @@ struct RenderJob {
     napi_ref out_ref[OUT_N] = {};
     void* out_ptr[OUT_N] = {};
     napi_ref caller_rgba = nullptr;  // settings.outRgba8
-    std::vector<uint8_t> preview;    // rt_output.preview_rgba8 (settings.preview)
+    uint8_t* frame = nullptr;        // rt_output.rgba8 when the caller gave outRgba8 (SceneBox::frame)
+    uint8_t* preview = nullptr;      // rt_output.preview_rgba8 (settings.preview; SceneBox::preview)
     int32_t preview_samples = 0;     // rt_output.preview_samples: the frame's samples (written by the worker)
-    int32_t shown_samples = -1;      // the frame last copied into the caller's imageData (main thread)
+    int32_t shown_samples = 0;       // the frame last copied into the caller's imageData (main thread)
     // progress hand-off: the worker waits until the main thread ran the JS callback
     std::mutex m;
     std::condition_variable cv;
@@ -240,9 +244,9 @@ uint8_t* live_bytes(napi_env env, napi_ref ref, size_t bytes) {
 void call_progress(napi_env env, napi_value js_cb, void*, void* data) {
     RenderJob* job = static_cast<RenderJob*>(data);     // alive: the worker waits for this call
     if (env) {
-        if (!job->preview.empty() && job->preview_samples != job->shown_samples)   // a newer frame only
-            if (uint8_t* dst = live_bytes(env, job->caller_rgba, job->preview.size())) {
-                std::memcpy(dst, job->preview.data(), job->preview.size());
+        if (job->preview && job->preview_samples != job->shown_samples)   // a newer frame only
+            if (uint8_t* dst = live_bytes(env, job->caller_rgba, job->n * 4)) {
+                std::memcpy(dst, job->preview, job->n * 4);
                 job->shown_samples = job->preview_samples;
             }
         if (js_cb) {
@@ -286,11 +290,11 @@ void execute(napi_env, void* data) {
     RenderJob* job = static_cast<RenderJob*>(data);
     rt_output out{};
     out.post = static_cast<float*>(job->out_ptr[RenderJob::OUT_POST]);
-    out.rgba8 = static_cast<uint8_t*>(job->out_ptr[RenderJob::OUT_RGBA]);
+    out.rgba8 = job->frame ? job->frame : static_cast<uint8_t*>(job->out_ptr[RenderJob::OUT_RGBA]);
     out.mean = static_cast<double*>(job->out_ptr[RenderJob::OUT_MEAN]);
     out.segments = static_cast<uint32_t*>(job->out_ptr[RenderJob::OUT_SEGS]);
     out.draws = static_cast<uint32_t*>(job->out_ptr[RenderJob::OUT_DRAWS]);
-    out.preview_rgba8 = job->preview.empty() ? nullptr : job->preview.data();
+    out.preview_rgba8 = job->preview;
     out.preview_samples = &job->preview_samples;
     const double t0 = trace_ms();
     if (t0 >= 0) fprintf(stderr, "[napi] rt_render start %.3f ms\n", t0);
@@ -333,10 +337,9 @@ void complete(napi_env env, napi_status, void* data) {
     if (job->tsfn) napi_release_threadsafe_function(job->tsfn, napi_tsfn_release);
     // the caller's imageData.data: the finished frame, or after a cancel the frame of the checkpointed
     // samples (rt_output.preview_rgba8); a buffer detached or transferred meanwhile fails the render
-    if (job->caller_rgba && (job->status == RT_OK || (job->status == RT_ERR_CANCELLED && !job->preview.empty()))) {
+    if (job->caller_rgba && (job->status == RT_OK || (job->status == RT_ERR_CANCELLED && job->preview))) {
         uint8_t* dst = live_bytes(env, job->caller_rgba, job->n * 4);
-        const uint8_t* src = job->status == RT_OK ? static_cast<const uint8_t*>(job->out_ptr[RenderJob::OUT_RGBA])
-                                                  : job->preview.data();
+        const uint8_t* src = job->status == RT_OK ? job->frame : job->preview;
         if (dst) std::memcpy(dst, src, job->n * 4);
         else if (job->status == RT_OK) {
             job->status = RT_ERR_INVALID;
@@ -451,14 +454,20 @@ napi_value render(napi_env env, napi_callback_info info) {
     // output buffers (see RenderJob): post unless settings.wantPost is 0; the RGBA8 frame also goes into
     // settings.outRgba8 when that is the frame's size; settings.preview: running frames into it too
     bool ok = !job->want_post || make_out(env, job, RenderJob::OUT_POST, job->n * 4 * sizeof(float));
-    if (ok) ok = make_out(env, job, RenderJob::OUT_RGBA, job->n * 4);
     void* rgba_p = nullptr;
     size_t rgba_bytes = 0;
     napi_value rgba_v;
     if (ok && get_bytes(env, s, "outRgba8", &rgba_p, &rgba_bytes) && rgba_bytes == job->n * 4 &&
         get_prop(env, s, "outRgba8", &rgba_v)) {
         ok = napi_create_reference(env, rgba_v, 1, &job->caller_rgba) == napi_ok;
-        if (ok && get_num(env, s, "preview", 0) != 0) job->preview.assign(job->n * 4, 0);
+        if (box->frame.size() != job->n * 4) box->frame.resize(job->n * 4);
+        job->frame = box->frame.data();
+        if (ok && get_num(env, s, "preview", 0) != 0) {
+            if (box->preview.size() != job->n * 4) box->preview.resize(job->n * 4);
+            job->preview = box->preview.data();
+        }
+    } else if (ok) {
+        ok = make_out(env, job, RenderJob::OUT_RGBA, job->n * 4);
     }
     if (ok && job->want_mean) ok = make_out(env, job, RenderJob::OUT_MEAN, job->n * 3 * sizeof(double));
     if (ok && job->want_counts) ok = make_out(env, job, RenderJob::OUT_SEGS, job->n * sizeof(uint32_t)) &&
