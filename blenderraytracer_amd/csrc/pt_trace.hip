@@ -40,11 +40,21 @@ struct TraceArgs {
 #endif
 
 #ifndef RT_SPHERES_WAVES_PER_SIMD
-#define RT_SPHERES_WAVES_PER_SIMD 5   // binary64 sphere-only walk (ACC_BVH_SPHERES): 96 VGPRs (4 / 5 waves: 7157 / 7407)
-#endif
+#define RT_SPHERES_WAVES_PER_SIMD 5   // binary64 sphere-only walk (ACC_BVH_SPHERES): 96 VGPRs, 13 spilled to
+#endif                                // scratch in cold paths; RTOW 128 spp 4 / 5 waves: 7119 / 7335 Msamples/s
 #ifndef RT_SPHERES_WAVES_F32
 #define RT_SPHERES_WAVES_F32 6       // binary32 sphere-only walk: 80 VGPRs (5 / 6 waves: 8536 / 8800 RTOW f32)
 #endif
+
+// the binary64 stack is static (24 entries) unless RT_F64_DYN_STACK (A/B): then, as binary32's, dynamic
+// LDS sized to the scene's deepest leaf, which 6 waves/SIMD would need.  Measured on the sphere-only
+// kernel, RTOW 512 spp: static 5 waves 7962, dynamic 5 waves 7870, dynamic 6 waves (57 VGPRs spilled)
+// 6909 Msamples/s
+#ifndef RT_F64_DYN_STACK
+#define RT_F64_DYN_STACK 0
+#endif
+template <class R, int ACC>
+constexpr bool dyn_stack() { return sizeof(R) == 4 || (RT_F64_DYN_STACK != 0 && ACC == ACC_BVH_SPHERES); }
 
 template <class R, int ACC>
 constexpr int waves_per_simd() {
@@ -98,7 +108,7 @@ void trace_kernel(const TraceArgs<R> args) {
     if constexpr (ACC >= ACC_BVH_STACK) {
         // per-lane traversal stacks, entry k of lane t at [k * 64 + t]: RT_BVH_STACK (binary64) or
         // sc.stack_entries (binary32: dynamic LDS sized by the launch to the scene's deepest leaf) x 4 B
-        if constexpr (sizeof(R) == 8) {
+        if constexpr (sizeof(R) == 8 && !dyn_stack<R, ACC>()) {
             __shared__ int bvh_stack[RT_BVH_STACK * 64];      // measured 1 % faster than the dynamic one
             stk.base = bvh_stack + threadIdx.x;
         } else {
@@ -175,7 +185,7 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
     } else if constexpr (ACC >= ACC_BVH_STACK) {
         // per-lane traversal stacks, entry k of lane t at [k * 64 + t]: RT_BVH_STACK (binary64) or
         // sc.stack_entries (binary32: dynamic LDS sized by the launch to the scene's deepest leaf) x 4 B
-        if constexpr (sizeof(R) == 8) {
+        if constexpr (sizeof(R) == 8 && !dyn_stack<R, ACC>()) {
             __shared__ int bvh_stack[RT_BVH_STACK * 64];      // measured 1 % faster than the dynamic one
             stk.base = bvh_stack + threadIdx.x;
         } else {
@@ -344,7 +354,7 @@ static int pool_chunk(int ns, int tiles, bool tri_bvh) {
 // dynamic LDS of a trace launch: the ordered walk's per-lane stacks (the scene's deepest leaf entries)
 template <int ACC, class R>
 static size_t stack_lds_bytes(const SceneView<R>& sc) {
-    return ACC >= ACC_BVH_STACK && sizeof(R) == 4 ? (size_t)std::min(sc.stack_entries, RT_BVH_STACK) * 64 * sizeof(int) : 0;
+    return ACC >= ACC_BVH_STACK && dyn_stack<R, ACC>() ? (size_t)std::min(sc.stack_entries, RT_BVH_STACK) * 64 * sizeof(int) : 0;
 }
 // ... of the pool kernel (RT_PARK: the parked path state + the stack, binary64)
 template <int ACC, class R>
