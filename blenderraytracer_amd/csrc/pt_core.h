@@ -86,7 +86,9 @@ struct SphereFilter { float cx, cy, cz, r2p; };
 template <class R> struct PlaneRec { R px, py, pz, nx, ny, nz; };
 template <class R> struct BoxRec { R mnx, mny, mnz, mxx, mxy, mxz; };
 template <class R> struct TriRec { R v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z, nx, ny, nz; };  // e1=v1-v0, e2=v2-v0
-template <class R> struct MatRec { int type, pad; R albedo[3]; R rough; R ior; R emit[3]; };
+// A material in 40 B (binary64): c = albedo (Lambertian, Metal) or emission = color * intensity
+// (Emissive), p = roughness (Metal) or refraction index (Dielectric) — a hit reads one record per segment
+template <class R> struct MatRec { int type, pad; R c[3]; R p; };
 // BVH leaf records in leaf order: everything one primitive test and its acceptance need (the
 // binary32 filter, the R-precision geometry, World index, World.objects index, material) in one
 // contiguous record, so a leaf issues all its loads at once instead of a chain of dependent ones.

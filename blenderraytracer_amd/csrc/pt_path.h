@@ -101,15 +101,15 @@ RT_HD R pow5_rn(R x) {
 template <class R>
 RT_HD bool scatter(const MatRec<R>& m, const Hit<R>& h, V3<R> unit, V3<R> p, Rng<R>& g, V3<R>& nd, V3<R>& att) {
     if (m.type <= 1) {
-        att = mk(m.albedo[0], m.albedo[1], m.albedo[2]);
+        att = mk(m.c[0], m.c[1], m.c[2]);
         if (m.type == 0) {                                                    // Lambertian :20-25
             nd = h.n + unit;
             return true;
         }
-        nd = reflect(unit, h.n) + p * m.rough;                                // Metal :36-41
+        nd = reflect(unit, h.n) + p * m.p;                                    // Metal :36-41 (roughness)
         return dot(nd, h.n) > (R)0;
     }
-    R ratio = h.front ? ((R)1 / m.ior) : m.ior;                               // Dielectric :51-83
+    R ratio = h.front ? ((R)1 / m.p) : m.p;                                   // Dielectric :51-83 (ior)
     R cos_t = js_min<R>(dot(unit * (R)-1, h.n), (R)1);
     R sin_t = sqrt((R)1 - cos_t * cos_t);
     bool reflect_it = ratio * sin_t > (R)1;
@@ -166,7 +166,7 @@ RT_HD bool shade_segment(const SceneView<R>& sc, const Closest<R>& c, V3<R>& o, 
     const V3<R> unit = normalize(hit && m.type == 0 ? p : d);
     if (hit) {
         if (m.type == 3) {                                                    // Emissive (materials.js:87-96)
-            L = mk(T.x * m.emit[0], T.y * m.emit[1], T.z * m.emit[2]);
+            L = mk(T.x * m.c[0], T.y * m.c[1], T.z * m.c[2]);                 // emission
         } else {
             V3<R> nd, att;
             if (scatter(m, h, unit, p, g, nd, att)) {

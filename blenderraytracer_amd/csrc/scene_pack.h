@@ -462,12 +462,9 @@ void make_records(const HostScene& hs, const rt_scene_desc& d, HostRecords<R>& o
         const rt_material_desc& m = d.materials[i];
         MatRec<R> r{};
         r.type = m.type;
-        for (int k = 0; k < 3; ++k) {
-            r.albedo[k] = (R)m.albedo[k];
-            r.emit[k] = (R)m.emission[k];
-        }
-        r.rough = (R)m.roughness;
-        r.ior = (R)m.ior;
+        const double* c = m.type == RT_MAT_EMISSIVE ? m.emission : m.albedo;
+        for (int k = 0; k < 3; ++k) r.c[k] = (R)c[k];
+        r.p = (R)(m.type == RT_MAT_METAL ? m.roughness : m.ior);
         out.mats[i] = r;
     }
     out.perm.assign(d.perm, d.perm + 512);
