@@ -429,11 +429,15 @@ struct Work {
 #define RT_COUNT(x) ((void)0)
 #endif
 
-// per-lane traversal stack of the ordered walk: entry k of this lane at base[k * stride] (LDS on the
-// GPU, strided by the workgroup size so a wave's accesses are conflict-free)
-struct BvhStack { int* base; int stride; };
-
 typedef float rt_f2 __attribute__((ext_vector_type(2)));
+typedef unsigned int rt_u2 __attribute__((ext_vector_type(2)));
+typedef unsigned int rt_u4 __attribute__((ext_vector_type(4)));
+
+// per-lane traversal stack of the ordered walk: entry k of this lane at base[k * stride] (LDS on the
+// GPU, strided by the workgroup size so a wave's accesses are conflict-free).  box / kid: the sphere
+// tree's nodes copied to LDS (ACC_BVH_SPHERES_LDS): node i's child boxes at box[3i .. 3i+2], its child
+// references at kid[i]
+struct BvhStack { int* base; int stride; const rt_u4* box = nullptr; const rt_u2* kid = nullptr; };
 
 #if defined(__HIP_DEVICE_COMPILE__)
 // IEEE 754-2019 minimum / maximum (v_minimum3_f32 / v_maximum3_f32 on gfx950): unlike fminf / fmaxf
@@ -472,7 +476,6 @@ RT_HD void bvh_node2_hit(const Bvh2Node& n, const BvhRay& r, float tlimit, bool&
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
-typedef unsigned int rt_u4 __attribute__((ext_vector_type(4)));
 // node i behind a raw buffer descriptor: 32-bit offsets, no 64-bit address arithmetic per node
 // (RTOW +1.4 %, f32 +2 %)
 __device__ __forceinline__ Bvh2Node load_node(__amdgpu_buffer_rsrc_t rs, int i) {
@@ -485,13 +488,26 @@ __device__ __forceinline__ Bvh2Node load_node(__amdgpu_buffer_rsrc_t rs, int i) 
 }
 #endif
 
+// node i from its LDS copy (three 16-B box reads, one 8-B reference read)
+RT_HD Bvh2Node load_node_lds(const BvhStack& s, int i) {
+    rt_u4 q[4];
+    q[0] = s.box[3 * i];
+    q[1] = s.box[3 * i + 1];
+    q[2] = s.box[3 * i + 2];
+    const rt_u2 k = s.kid[i];
+    q[3] = rt_u4{k.x, k.y, 0u, 0u};
+    Bvh2Node n;
+    memcpy(&n, q, sizeof n);
+    return n;
+}
+
 // Walk one BVH and call leaf(fc) for every leaf whose box the ray reaches before the current best.
 // WIDE: ordered walk over Bvh2Node (both child boxes per 64-B node, nearer child first, the other
 // pushed on the lane's stack); otherwise the stackless preorder walk over BvhNode skip links (A/B and
 // host cross-check).  Variants measured slower and removed: postponed leaves,
 // "while-while" leaf batching, binary16 child boxes, four-child nodes, stack top in a register, leaf
 // records as buffer loads.
-template <bool WIDE, class Leaf>
+template <bool WIDE, bool LDSN = false, class Leaf>
 RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const BvhRay& br, const float& tl,
                     BvhStack stk, Work& w, Leaf&& leaf) {
     if constexpr (WIDE) {
@@ -533,9 +549,10 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
                 // every active lane at the same node (30 % of RTOW walk steps, 49 % on mesh50k): read
                 // it with scalar loads, which bypass the vector memory pipeline (+3.5 %)
                 const int first = __builtin_amdgcn_readfirstlane(cur);
-                down = __ballot(cur != first) == 0 ? step(wide[first]) : step(load_node(wrs, cur));
+                if constexpr (LDSN) down = __ballot(cur != first) == 0 ? step(wide[first]) : step(load_node_lds(stk, cur));
+                else down = __ballot(cur != first) == 0 ? step(wide[first]) : step(load_node(wrs, cur));
 #else
-                down = step(wide[cur]);
+                down = step(LDSN ? load_node_lds(stk, cur) : wide[cur]);
 #endif
                 if (down) continue;
             } else {
@@ -635,7 +652,8 @@ RT_HD void tri_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R tmin, Cl
 // records are contiguous in leaf order.  WIDE: the ordered two-child walk (default); else the
 // stackless preorder walk.
 // TRI = false (ACC_BVH_SPHERES): scenes without triangles; the triangle walk's code is left out.
-template <class R, bool WIDE, bool TRI = true>
+// LDSN: the sphere tree's nodes are read from their LDS copy in stk (ACC_BVH_SPHERES_LDS).
+template <class R, bool WIDE, bool TRI = true, bool LDSN = false>
 RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
     const R tmin = (R)0.001;
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
@@ -650,7 +668,7 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
         if (sc.num_big_spheres > 0) sphere_records(sc.big_spheres, 0, sc.num_big_spheres, o, d, a, fr, tmin, b, tl, w, true);
         auto leaf = [&](int fc) { sphere_leaf(sc, fc, o, d, a, fr, tmin, b, tl, w); };
         if (sc.num_sphere_nodes > 0)
-            bvh_walk<WIDE>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w, leaf);
+            bvh_walk<WIDE, LDSN>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w, leaf);
     }
     if (TRI && sc.num_tri_nodes > 0) {
         auto leaf = [&](int fc) { tri_leaf(sc, fc, o, d, tmin, b, tl, w); };
@@ -662,13 +680,15 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
 // acceleration modes of the trace kernel
 // ACC_BVH_SPHERES: the ordered walk for scenes without triangles (sphere tree + planes/boxes only): the
 // kernel then holds no triangle-test code, and its binary64 form fits 5 waves/SIMD (RTOW +1.7 %)
-enum Accel : int { ACC_BRUTE = 0, ACC_BVH = 2, ACC_BVH_STACK = 3, ACC_BVH_SPHERES = 4 };
+// ACC_BVH_SPHERES_LDS: the same walk with the sphere tree's nodes in LDS (trace_pool_lds_kernel)
+enum Accel : int { ACC_BRUTE = 0, ACC_BVH = 2, ACC_BVH_STACK = 3, ACC_BVH_SPHERES = 4, ACC_BVH_SPHERES_LDS = 5 };
 
 template <class R, int ACC>
 RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
     if constexpr (ACC == ACC_BVH) return closest_hit_bvh<R, false>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_BVH_STACK) return closest_hit_bvh<R, true>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_BVH_SPHERES) return closest_hit_bvh<R, true, false>(sc, o, d, w, stk);
+    else if constexpr (ACC == ACC_BVH_SPHERES_LDS) return closest_hit_bvh<R, true, false, true>(sc, o, d, w, stk);
     else return closest_hit<R>(sc, o, d);
 }
 

@@ -11,6 +11,7 @@
 // brute-force mode: primitive records are walked in World.objects order by every lane in lockstep, so
 // all record loads are wave-uniform scalar loads.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -56,9 +57,17 @@ struct TraceArgs {
 template <class R, int ACC>
 constexpr bool dyn_stack() { return sizeof(R) == 4 || (RT_F64_DYN_STACK != 0 && ACC == ACC_BVH_SPHERES); }
 
+#ifndef RT_LDS_OCC_F64
+#define RT_LDS_OCC_F64 4          // waves/SIMD of the LDS-node kernel (trace_pool_lds_kernel)
+#endif
+#ifndef RT_LDS_OCC_F32
+#define RT_LDS_OCC_F32 6
+#endif
+
 template <class R, int ACC>
 constexpr int waves_per_simd() {
     if constexpr (ACC == ACC_BVH_SPHERES) return sizeof(R) == 8 ? RT_SPHERES_WAVES_PER_SIMD : RT_SPHERES_WAVES_F32;
+    if constexpr (ACC == ACC_BVH_SPHERES_LDS) return sizeof(R) == 8 ? RT_LDS_OCC_F64 : RT_LDS_OCC_F32;
     return ACC >= ACC_BVH ? (sizeof(R) == 8 ? RT_BVH_WAVES_PER_SIMD : RT_BVH_WAVES_F32) : RT_MIN_WAVES_PER_SIMD;
 }
 
@@ -296,6 +305,181 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
     add_totals<ACC>(args.c, res, lane);
 }
 
+// One (tile, chunk) item of the pool in a multi-wave workgroup (trace_pool_lds_kernel): item = chunk *
+// tiles + tile, traced exactly as trace_pool_kernel traces its workgroup's item.  acc: the wave's
+// 3 x 64 LDS partials (zero on entry, zero again on return); the barriers around them are wave-local.
+// (trace_pool_kernel keeps its own copy of this loop: calling this function from it measured -1.6 %
+// on RTOW binary64, from a different register allocation.)
+template <class R, bool COUNT, int ACC>
+__device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __restrict__ part, const int tiles,
+                                          const int chunk, const unsigned item, double* acc, BvhStack stk,
+                                          PixelResult& res, const int lane) {
+    const ImageParams& im = args.im;
+    const SceneView<R>& sc = args.sc;
+    const int ci = item / tiles, tile = item % tiles;     // (unsigned, as blockIdx.x)
+    const Tile tl = tile_of(im, tile);
+    const int vw = tl.vw, nv = tl.nv;
+    const int sb = im.s_begin + ci * chunk, se = min(im.s_end, sb + chunk);
+    const uint32_t total = (uint32_t)nv * (uint32_t)max(0, se - sb);
+    // the lane's current item: pixel m of the tile = (i, j) with key pkey at crop index q, sample s
+    int i = 0, j = 0, s = 0, depth = 0;
+    uint32_t m = 0, pkey = 0, isegs = 0;
+    size_t q = 0;
+    Rng<R> g;
+    V3<R> o, d, T;
+    auto begin_item = [&](const uint32_t k) {
+        uint32_t sr;
+        if (nv == 64) { m = k & 63; sr = k >> 6; }
+        else { sr = k / (uint32_t)nv; m = k - sr * (uint32_t)nv; }
+        const int px = tl.x0 + (int)(m % (uint32_t)vw), py = tl.y0 + (int)(m / (uint32_t)vw);
+        const int row = im.y0 + py;
+        i = im.x0 + px;
+        j = im.height - 1 - row;
+        pkey = pixel_key(im.seedm, (uint32_t)row * (uint32_t)im.width + (uint32_t)i);
+        q = (size_t)py * im.cw + px;
+        s = sb + (int)sr;
+        T = mk<R>(1, 1, 1);
+        depth = im.max_depth;
+        isegs = 0;
+        start_sample(sc, im, i, j, pkey, s, g, o, d);
+    };
+    uint32_t next = 64;                       // items [0, 64) are dealt to lanes 0..63 up front
+    bool live = (uint32_t)lane < total;
+    if (live) begin_item((uint32_t)lane);
+    while (live) {                            // lanes only ever leave this loop, so every live lane
+        const uint64_t t0 = RT_TICK();        // has seen every update of `next`
+        const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, res.work, stk);
+        const uint64_t t1 = RT_TICK();
+        if (RT_PROFILE) res.cyc[0] += t1 - t0;
+        ++res.segments;
+        ++isegs;
+        V3<R> L;
+        const bool done = shade_segment(sc, c, o, d, T, depth, g, L);
+        const uint64_t t2 = RT_TICK();
+        if (RT_PROFILE) res.cyc[1] += t2 - t1;
+        const uint64_t need = __ballot(done);
+        if (need) {
+            if (COUNT && done) {
+                if (args.c.segs) atomicAdd(args.c.segs + q, isegs);
+                if (args.c.draws) atomicAdd(args.c.draws + q, g.k);
+            }
+            // add the finished samples' radiance to its pixel's partial: non-returning LDS atomics
+            // (ds_add_f64), no wait.  Lanes that finish samples of the same pixel in one iteration
+            // are combined by the LDS atomic unit in its fixed lane order.
+            if (done) {
+                __hip_atomic_fetch_add(&acc[m], (double)L.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&acc[64 + m], (double)L.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&acc[128 + m], (double)L.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if (done) {
+                const uint32_t k = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0));
+                live = k < total;
+                if (live) begin_item(k);
+            }
+            next += (uint32_t)__popcll(need);
+        }
+        if (RT_PROFILE) res.cyc[2] += RT_TICK() - t2;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane < nv) {
+        if (part) {
+            double* p = part + ((size_t)item * 3) * 64 + lane;           // item = chunk * tiles + tile
+            p[0] = acc[lane];
+            p[64] = acc[64 + lane];
+            p[128] = acc[128 + lane];
+        } else {                                  // the launch's only chunk: this wave owns the pixels
+            const size_t qq = (size_t)(tl.y0 + lane / vw) * im.cw + (tl.x0 + lane % vw);
+            args.c.sum[3 * qq] += acc[lane];
+            args.c.sum[3 * qq + 1] += acc[64 + lane];
+            args.c.sum[3 * qq + 2] += acc[128 + lane];
+        }
+    }
+    acc[lane] = 0;                            // the wave's next item starts from zero partials
+    acc[64 + lane] = 0;
+    acc[128 + lane] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// ---- sample pool with the sphere tree's nodes in LDS (ACC_BVH_SPHERES_LDS) ----
+// The walk's divergent node reads (4 x 16 B per lane and step through the vector memory path, which
+// is ~0.86 busy on RTOW) become LDS reads: a workgroup of lds_waves() waves copies the
+// scene's two-child nodes into LDS once — child boxes (48 B, three 16-B reads at a 48-B stride, which
+// spreads a 16-lane group's reads over 16 bank groups) and child references (8 B) in separate arrays —
+// and its waves then take (tile, chunk) items from a device-wide queue until it is empty, so the
+// workgroup's waves finish together and the copy is paid once per workgroup, not per item.  The items
+// are the one-wave kernel's (item = chunk * tiles + tile, same partials layout), and each is traced
+// exactly as there, so the sums are bit-identical to it.  The queue is one of kPoolQueues counter
+// pairs {next item, waves exited} (a ring, one per launch): the last wave to exit sets both back to 0.
+// Waves per workgroup: a multiple of 4, so that every workgroup puts the same number of waves on
+// each SIMD (10-wave workgroups at 5 waves/SIMD left one SIMD a wave short of the second workgroup:
+// one workgroup per CU, RTOW -28 %)
+#ifndef RT_LDS_WAVES_F64
+#define RT_LDS_WAVES_F64 8        // 2 workgroups per CU at 4 waves/SIMD
+#endif
+#ifndef RT_LDS_WAVES_F32
+#define RT_LDS_WAVES_F32 12       // 2 workgroups per CU at 6 waves/SIMD
+#endif
+template <class R>
+constexpr int lds_waves() { return sizeof(R) == 8 ? RT_LDS_WAVES_F64 : RT_LDS_WAVES_F32; }
+constexpr int kPoolQueues = 1024;
+__device__ uint32_t g_pool_queue[2 * kPoolQueues];
+
+// the sphere tree's two-child nodes into LDS: child boxes at box[3k .. 3k+2], references at kid[k]
+template <class R>
+__device__ __forceinline__ void copy_nodes_lds(const SceneView<R>& sc, rt_u4* box, rt_u2* kid, int t, int threads) {
+    for (int k = t; k < sc.num_sphere_wide; k += threads) {
+        const rt_u4* g = reinterpret_cast<const rt_u4*>(sc.sphere_wide + k);
+        const rt_u4 q3 = g[3];
+        box[3 * k] = g[0];
+        box[3 * k + 1] = g[1];
+        box[3 * k + 2] = g[2];
+        kid[k] = rt_u2{q3.x, q3.y};
+    }
+}
+
+template <class R, bool COUNT>
+__global__ __launch_bounds__(64 * lds_waves<R>(), (waves_per_simd<R, ACC_BVH_SPHERES_LDS>()))
+void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, const int tiles, const int chunk,
+                           const int items, const int qi) {
+    constexpr int ACC = ACC_BVH_SPHERES_LDS, W = lds_waves<R>();
+    const SceneView<R>& sc = args.sc;
+    // dynamic LDS: [child boxes 48 B x n][child references 8 B x n][W stacks of entries x 64 ints]
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_dyn[];
+    __shared__ double acc_all[W * 3 * 64];
+    const int n = sc.num_sphere_wide, entries = min(sc.stack_entries, RT_BVH_STACK);
+    rt_u4* box = reinterpret_cast<rt_u4*>(lds_dyn);
+    rt_u2* kid = reinterpret_cast<rt_u2*>(lds_dyn + 48 * n);
+    int* stacks = reinterpret_cast<int*>(lds_dyn + 56 * n);
+    copy_nodes_lds(sc, box, kid, threadIdx.x, 64 * W);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double* acc = acc_all + wave * 3 * 64;
+    acc[lane] = 0;
+    acc[64 + lane] = 0;
+    acc[128 + lane] = 0;
+    __syncthreads();
+    const BvhStack stk{stacks + wave * entries * 64 + lane, 64, box, kid};
+    uint32_t* queue = g_pool_queue + 2 * qi;
+    PixelResult res{0, 0, {0, 0, 0}, {0, 0, 0}};
+    for (;;) {
+        uint32_t it = 0;
+        if (lane == 0) it = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        it = (uint32_t)__builtin_amdgcn_readfirstlane((int)it);
+        if (it >= (uint32_t)items) break;
+        pool_item<R, COUNT, ACC>(args, part, tiles, chunk, it, acc, stk, res, lane);
+    }
+    add_totals<ACC>(args.c, res, lane);
+    if (lane == 0) {
+        const uint32_t e = __hip_atomic_fetch_add(queue + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (e == gridDim.x * W - 1) {      // every other wave has made its last queue read
+            __hip_atomic_store(queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(queue + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 // sum[q] += part[c][tile][.][m] for c = 0 .. chunks-1 in chunk order (binary64); one thread per pixel,
 // one one-wave workgroup per tile (its reads of one chunk are 3 x 512 contiguous bytes).  One-wave
 // workgroups: while the next batch's trace waves hold the CUs (overlapped batches), a 256-thread
@@ -373,9 +557,54 @@ size_t pool_partial_bytes(int cw, int ch, int ns, bool tri_bvh, int chunk_overri
     return chunks > 1 ? chunks * tiles * kPartialBytesPerTile : 0;
 }
 
+// Which sphere-only launches read the nodes from LDS: binary32 (RTOW 256 spp, 6 waves/SIMD: 9752 vs
+// 9504 Msamples/s); binary64 only when asked (RT_LDS_NODES=2): RTOW's 481 nodes (27 KB) + 5 workgroups'
+// stacks and partials exceed 160 KiB at 5 waves/SIMD, and at 4 the LDS kernel (7497) is slower than the
+// one-wave kernel at 5 (7744; at 4: 7291).  RT_LDS_NODES=0: never (A/B).
+#ifndef RT_LDS_NODES
+#define RT_LDS_NODES 1
+#endif
+// LDS of trace_pool_lds_kernel (dynamic part), 0 if not used for this scene or if its sphere tree does
+// not fit: the kernel's workgroups per CU share its 160 KiB
+template <class R>
+static size_t lds_nodes_bytes(const SceneView<R>& sc) {
+    static int v = -1;
+    if (v == -1) {
+        const char* e = getenv("RT_LDS_NODES");
+        v = e ? atoi(e) : RT_LDS_NODES;
+    }
+    if (v < (sizeof(R) == 8 ? 2 : 1) || sc.num_sphere_wide <= 0) return 0;
+    constexpr int W = lds_waves<R>();
+    const size_t b = (size_t)56 * sc.num_sphere_wide + (size_t)W * std::min(sc.stack_entries, RT_BVH_STACK) * 64 * 4;
+    const size_t budget = 160 * 1024 / (4 * waves_per_simd<R, ACC_BVH_SPHERES_LDS>() / W);
+    return b + (size_t)W * 3 * 64 * 8 + 256 <= budget ? b : 0;
+}
+
+static int device_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus[dev] = 256;
+    return cus[dev];
+}
+
 template <class R, int ACC>
 static void launch_pool_kernel(const TraceArgs<R>& a, bool count, double* part, int tiles, int chunks, int chunk,
                                hipStream_t stream) {
+    if constexpr (ACC == ACC_BVH_SPHERES) {
+        const size_t lb = lds_nodes_bytes(a.sc);
+        if (lb) {
+            static std::atomic<unsigned> next_queue{0};
+            const int qi = (int)(next_queue++ % kPoolQueues);
+            const long long items = (long long)tiles * chunks;
+            constexpr int W = lds_waves<R>();
+            const int resident = device_cus() * 4 * waves_per_simd<R, ACC_BVH_SPHERES_LDS>() / W;
+            const int grid = (int)std::min<long long>(resident, (items + W - 1) / W);
+            if (count) hipLaunchKernelGGL((trace_pool_lds_kernel<R, true>), dim3(grid), dim3(64 * W), lb, stream, a, part, tiles, chunk, (int)items, qi);
+            else hipLaunchKernelGGL((trace_pool_lds_kernel<R, false>), dim3(grid), dim3(64 * W), lb, stream, a, part, tiles, chunk, (int)items, qi);
+            return;
+        }
+    }
     const size_t lds = pool_lds_bytes<ACC>(a.sc);
     if (count) hipLaunchKernelGGL((trace_pool_kernel<R, true, ACC>), dim3(tiles * chunks), dim3(64), lds, stream, a, part, tiles, chunk);
     else hipLaunchKernelGGL((trace_pool_kernel<R, false, ACC>), dim3(tiles * chunks), dim3(64), lds, stream, a, part, tiles, chunk);
@@ -518,12 +747,39 @@ __global__ __launch_bounds__(64) void closest_hits_kernel(const SceneView<R> sc,
     idx_out[r] = c.kind == HIT_NONE ? -1 : c.idx;
 }
 
+// ... through the LDS copy of the nodes (the walk of trace_pool_lds_kernel)
+template <class R>
+__global__ __launch_bounds__(64) void closest_hits_lds_kernel(const SceneView<R> sc, const double* __restrict__ rays,
+                                                              const size_t n, double* __restrict__ t_out,
+                                                              int* __restrict__ kind_out, int* __restrict__ idx_out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_dyn[];   // [boxes][references][stack]
+    const int nn = sc.num_sphere_wide;
+    rt_u4* box = reinterpret_cast<rt_u4*>(lds_dyn);
+    rt_u2* kid = reinterpret_cast<rt_u2*>(lds_dyn + 48 * nn);
+    copy_nodes_lds(sc, box, kid, threadIdx.x, 64);
+    __syncthreads();
+    const BvhStack stk{reinterpret_cast<int*>(lds_dyn + 56 * nn) + threadIdx.x, 64, box, kid};
+    const size_t r = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (r >= n) return;
+    const double* q = rays + 6 * r;
+    const V3<R> o = mk<R>((R)q[0], (R)q[1], (R)q[2]), d = mk<R>((R)q[3], (R)q[4], (R)q[5]);
+    Work w{0, 0, 0, 0, 0, 0};
+    const Closest<R> c = closest_hit_acc<R, ACC_BVH_SPHERES_LDS>(sc, o, d, w, stk);
+    t_out[r] = c.kind == HIT_NONE ? (double)INFINITY : (double)c.t;
+    kind_out[r] = c.kind;
+    idx_out[r] = c.kind == HIT_NONE ? -1 : c.idx;
+}
+
 template <class R>
 hipError_t launch_closest_hits(const SceneView<R>& sc, bool bvh, const double* rays, size_t n, double* t, int* kind,
                                int* idx, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 63) / 64));
-    if (bvh && bvh_walk_mode(sc) == ACC_BVH_SPHERES)   // the walk the trace kernel runs on this scene
+    const bool spheres = bvh && bvh_walk_mode(sc) == ACC_BVH_SPHERES;   // the walk the trace kernel runs
+    if (spheres && lds_nodes_bytes(sc)) {
+        const size_t lb = (size_t)56 * sc.num_sphere_wide + (size_t)std::min(sc.stack_entries, RT_BVH_STACK) * 64 * 4;
+        hipLaunchKernelGGL((closest_hits_lds_kernel<R>), grid, dim3(64), lb, stream, sc, rays, n, t, kind, idx);
+    } else if (spheres)
         hipLaunchKernelGGL((closest_hits_kernel<R, ACC_BVH_SPHERES>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);
     else if (bvh) hipLaunchKernelGGL((closest_hits_kernel<R, ACC_BVH_STACK>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);
     else hipLaunchKernelGGL((closest_hits_kernel<R, ACC_BRUTE>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);

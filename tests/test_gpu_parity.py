@@ -347,6 +347,21 @@ def test_sample_pool_vs_lane_per_pixel(gpu, tmp_path, env):
             assert np.allclose(base[k][ok], pool[k][ok], rtol=SUM_RTOL, atol=1e-300), k
 
 
+@pytest.mark.parametrize("env", [{}, {"RT_PART_MB": "1", "RT_POOL_CHUNK": "2"}], ids=["default", "split_launches"])
+def test_lds_node_kernel_bit_identical(gpu, tmp_path, env):
+    """trace_pool_lds_kernel (sphere tree nodes in LDS, multi-wave workgroups taking (tile, chunk)
+    items from a device-wide queue; default for binary32 sphere scenes, RT_LDS_NODES=2 forces it for
+    binary64 too) renders exactly the bits of the one-wave pool kernel (RT_LDS_NODES=0): sums, segment
+    and draw counts, batched renders — also over many launches (1-MiB partials budget, 2-sample chunks:
+    the queue ring is reused) and in a second process."""
+    base = _render_in_child(_POOL_SCRIPT, tmp_path / "global.npz", RT_LDS_NODES="0", **env)
+    lds = _render_in_child(_POOL_SCRIPT, tmp_path / "lds.npz", RT_LDS_NODES="2", **env)
+    again = _render_in_child(_POOL_SCRIPT, tmp_path / "again.npz", RT_LDS_NODES="2", **env)
+    for k in base.files:
+        assert np.array_equal(base[k], lds[k], equal_nan=True), k
+        assert np.array_equal(lds[k], again[k], equal_nan=True), k
+
+
 def test_trace_device_two_streams_then_render(gpu):
     """Scene scratch shared across streams: two rt_trace_device shards enqueued on two
     different streams with no host synchronization, then rt_render on the scene's own stream: every
