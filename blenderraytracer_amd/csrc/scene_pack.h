@@ -482,7 +482,7 @@ void make_records(const HostScene& hs, const rt_scene_desc& d, HostRecords<R>& o
     for (int id : hs.tri_bvh_prims) {
         const TriRec<R>& r = out.tris[id];
         out.bvh_tri_leaf.push_back(TriLeaf<R>{{r.v0x, r.v0y, r.v0z, r.e1x, r.e1y, r.e1z, r.e2x, r.e2y, r.e2z},
-                                              id, hs.tri_obj[id], hs.tri_mat[id], 0});
+                                              id, hs.tri_obj[id]});
     }
 }
 
