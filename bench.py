@@ -163,7 +163,9 @@ def cpu_baseline(rt, cfg_name, cfg, seed, side):
 # VALU issue ceiling: 256 CUs x 4 SIMD-32s, a wave64 VALU instruction holds its SIMD for 2 cycles (a
 # binary64 one for 4: FP64 vector is half the FP32 rate) at 2.4 GHz (MI355X_MICROARCH.md)
 VALU_ISSUE_PEAK_GSLOTS = 256 * 4 * 2.4 / 2
-TRACE_KERNELS = ("trace_pool_kernel", "reduce_kernel")   # the trace step: one launch each per frame
+# the trace step: one launch each per frame ("trace_pool": trace_pool_kernel, or trace_pool_lds_kernel for
+# binary32 sphere scenes)
+TRACE_KERNELS = ("trace_pool", "reduce_kernel")
 # the vector-memory data path (TA address / TD data units, vector L1 = TCP, L2 = TCC): TA 1 of 2, TD 1 of 2,
 # TCP 2 of 4, TCC 2 of 4, GRBM 1 of 2 counters per pass
 VMEM_COUNTERS = ("TA_TA_BUSY_sum", "TD_TD_BUSY_sum", "TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum",
@@ -387,7 +389,8 @@ def main():
         else:
             flops = seg_launch * flops_per_segment
         rank_samples = cfg["w"] * cfg["h"] * (job.range[1] - job.range[0])
-        kernel_desc = "trace step: trace_pool_kernel + reduce_kernel (one launch each per frame)"
+        kernel_desc = ("trace step: trace_pool_kernel (trace_pool_lds_kernel for binary32 sphere scenes) + "
+                       "reduce_kernel (one launch each per frame)")
         roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                     "traffic": None, "kernel": kernel_desc, "kernel_ms": round(k_ms, 3)}
         binding = vmem = None
@@ -428,13 +431,13 @@ def main():
                            "waves_per_launch": sq.get("SQ_WAVES"),
                            "source": "rocprofv3 --pmc SQ_* pass over one frame run by this bench invocation / this "
                                      "run's HIP-event trace-step time"}
-                vm = pmc["vmem"]["per_kernel"].get("trace_pool_kernel", {})
+                vm = pmc["vmem"]["per_kernel"].get("trace_pool", {})
                 grbm = vm.get("GRBM_GUI_ACTIVE", 0.0)
                 cu_cycles = 256 * grbm / 8       # rocprofv3's GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles
                 if cu_cycles > 0:
                     acc = vm.get("TCP_TOTAL_CACHE_ACCESSES_sum", 0.0)
                     hit, miss = vm.get("TCC_HIT_sum", 0.0), vm.get("TCC_MISS_sum", 0.0)
-                    vmem = {"bound": "vector_memory", "kernel": "trace_pool_kernel",
+                    vmem = {"bound": "vector_memory", "kernel": "trace_pool_kernel / trace_pool_lds_kernel",
                             "td_busy": round(vm.get("TD_TD_BUSY_sum", 0.0) / cu_cycles, 4),
                             "ta_busy": round(vm.get("TA_TA_BUSY_sum", 0.0) / cu_cycles, 4),
                             "l1_hit": round(1 - vm.get("TCP_TCC_READ_REQ_sum", 0.0) / acc, 4) if acc else None,

@@ -5,7 +5,7 @@ pre=$1; shift
 for t in "$@"; do
   src=gpurun_out/prof_$t
   cp $src/kt/run_kernel_stats.csv profiles/${pre}_${t}_kernel_stats.csv
-  grep -E '^"Kind"|trace_pool_kernel|reduce_kernel' $src/kt/run_kernel_trace.csv > profiles/${pre}_${t}_kernel_trace.csv
+  grep -E '^"Kind"|trace_pool_(lds_)?kernel|reduce_kernel' $src/kt/run_kernel_trace.csv > profiles/${pre}_${t}_kernel_trace.csv
   tail -1 $src/bench.json > profiles/${pre}_${t}_bench.json
   for p in fetch write sq vmem; do
     f=$(find $src/pmc/$p -name '*counter_collection.csv' | head -1)
