@@ -421,6 +421,7 @@ RT_HD bool bvh_node_hit(const BvhNode& n, const BvhRay& r, float tlimit) {
 struct Work {
     uint32_t nodes, spheres, tris;                // BVH nodes visited, sphere / triangle tests (stats)
     uint32_t lane_trips, wave_trips, uni_trips;   // RT_PROFILE: walk iterations per lane / per wave / uniform
+    uint32_t low8, low16;                         // RT_PROFILE: wave iterations with <= 8 / <= 16 lanes walking
 };
 #ifndef RT_BVH_COUNT
 #define RT_BVH_COUNT 1            // 0 measured slower (-2 % RTOW, -9 % mesh50k: worse register allocation)
@@ -537,7 +538,12 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
         for (;;) {
 #if RT_PROFILE && defined(__HIP_DEVICE_COMPILE__)
             ++w.lane_trips;                       // the first active lane counts the wave's iteration
-            if ((int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) ++w.wave_trips;
+            const int act = __popcll(__ballot(1));
+            if ((int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) {
+                ++w.wave_trips;
+                if (act <= 8) ++w.low8;
+                if (act <= 16) ++w.low16;
+            }
             {   // iterations in which every active lane is at the same inner node
                 const int first = __builtin_amdgcn_readfirstlane(cur);
                 const bool uni = __ballot(cur != first) == 0 && first >= 0;

@@ -9,7 +9,7 @@ namespace rt {
 
 // Counters::totals slots: 0 segments, 1 BVH nodes, 2 sphere tests, 3 triangle tests; RT_PROFILE builds:
 // 4..6 cycles (closest hit, shading, regeneration), 7 / 8 walk iterations per lane / per wave, 9 wave
-// iterations whose active lanes all sit at one inner node
+// iterations whose active lanes all sit at one inner node, 10 / 11 wave iterations with <= 8 / <= 16 lanes walking
 constexpr int kTotalSlots = 12;
 
 // chunk partial sums of one 8x8 tile: 3 channels x 64 pixels, binary64

@@ -87,8 +87,8 @@ __device__ __forceinline__ void add_totals(const Counters& c, const PixelResult&
             for (int off = 32; off > 0; off >>= 1) v = max(v, (unsigned long long)__shfl_xor(v, off));
             if (lane == 0) atomicAdd(c.totals + 4 + k, v);
         }
-        const uint32_t trips[3] = {r.work.lane_trips, r.work.wave_trips, r.work.uni_trips};
-        for (int k = 0; k < 3; ++k) {
+        const uint32_t trips[5] = {r.work.lane_trips, r.work.wave_trips, r.work.uni_trips, r.work.low8, r.work.low16};
+        for (int k = 0; k < 5; ++k) {
             unsigned long long v = trips[k];
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
             if (lane == 0) atomicAdd(c.totals + 7 + k, v);

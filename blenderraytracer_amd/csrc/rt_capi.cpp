@@ -917,6 +917,8 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
             totals[4] / cyc, totals[5] / cyc, totals[6] / cyc, cyc, (double)totals[7], (double)totals[8],
             totals[8] ? (double)totals[7] / (64.0 * (double)totals[8]) : 0.0,
             totals[8] ? (double)totals[9] / (double)totals[8] : 0.0);
+    fprintf(stderr, "[rt_profile] wave walk iterations with <= 8 lanes walking %.3f, <= 16 %.3f\n",
+            totals[8] ? (double)totals[10] / (double)totals[8] : 0.0, totals[8] ? (double)totals[11] / (double)totals[8] : 0.0);
 #endif
     return RT_OK;
 }
