@@ -580,6 +580,10 @@ static size_t lds_nodes_bytes(const SceneView<R>& sc) {
     return b + (size_t)W * 3 * 64 * 8 + 256 <= budget ? b : 0;
 }
 
+// the next queue of the ring: one counter for every instantiation and thread, so launches in flight
+// together (streams, scenes, precisions) never share a queue
+static std::atomic<unsigned> g_next_queue{0};
+
 static int device_cus() {
     static int cus[64] = {0};
     int dev = 0;
@@ -594,8 +598,7 @@ static void launch_pool_kernel(const TraceArgs<R>& a, bool count, double* part, 
     if constexpr (ACC == ACC_BVH_SPHERES) {
         const size_t lb = lds_nodes_bytes(a.sc);
         if (lb) {
-            static std::atomic<unsigned> next_queue{0};
-            const int qi = (int)(next_queue++ % kPoolQueues);
+            const int qi = (int)(g_next_queue++ % kPoolQueues);
             const long long items = (long long)tiles * chunks;
             constexpr int W = lds_waves<R>();
             const int resident = device_cus() * 4 * waves_per_simd<R, ACC_BVH_SPHERES_LDS>() / W;

@@ -362,12 +362,14 @@ def test_lds_node_kernel_bit_identical(gpu, tmp_path, env):
         assert np.array_equal(lds[k], again[k], equal_nan=True), k
 
 
-def test_trace_device_two_streams_then_render(gpu):
+@pytest.mark.parametrize("precision", [capi.RT_PREC_F64, capi.RT_PREC_F32], ids=["f64", "f32"])
+def test_trace_device_two_streams_then_render(gpu, precision):
     """Scene scratch shared across streams: two rt_trace_device shards enqueued on two
     different streams with no host synchronization, then rt_render on the scene's own stream: every
-    result equals its single-launch counterpart."""
+    result equals its single-launch counterpart.  In binary32 the launches are trace_pool_lds_kernel's,
+    running at once on the two streams, each with its own device-wide item queue."""
     import torch
-    rt = _rtow(200, 120, 24)            # several chunks per launch: the shards use the partials buffer
+    rt = _rtow(200, 120, 24, precision=precision)   # several chunks per launch: the shards use the partials buffer
     lib = capi.load_library()
     scene = rt.scene_handle()
     n = 200 * 120
