@@ -148,6 +148,15 @@ struct SceneView {
     int stack_entries;             // deepest leaf of the two trees (>= 1): the ordered walk's stack bound
     const SphereLeaf<R>* big_spheres;   // dominant spheres kept out of the sphere tree (scene_pack.h)
     int num_big_spheres;
+    // uniform grid over the sphere tree's spheres (ACC_GRID, scene_pack.h build_grid): cell c = (x, y, z)
+    // -> x + n0 (y + n1 z) holds grid_leaf[grid_cell[c] .. grid_cell[c + 1])
+    const int* grid_cell;
+    const SphereLeaf<R>* grid_leaf;
+    int grid_n[3];
+    float grid_lo[3], grid_hi[3], grid_cs[3];   // cells [lo + k cs, lo + (k+1) cs); hi: the padded box
+    float grid_far;                // rays with |origin|_inf beyond this take the sphere-list fallback
+    int num_grid_cells;            // 0: no grid
+    int use_grid;                  // choose_walk (scene_pack.h): the trace kernel walks the grid
     // camera (camera.js:8-36 vectors, computed on the host in binary64)
     R cam_o[3], cam_llc[3], cam_h[3], cam_v[3], cam_u[3], cam_vv[3], cam_w[3];
     R lens_radius;
@@ -685,11 +694,94 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
     return b;
 }
 
+// Closest hit through the uniform grid (sphere-only scenes): planes and boxes brute force, the dominant
+// spheres, then the cells the ray crosses in order of t (3D-DDA in binary32), every sphere registered
+// in a cell tested as in a BVH leaf, until the best hit lies before the exit of the current cell.
+// grid_bound: a sphere is registered in every cell its box, padded by m (scene_pack.h build_grid),
+// overlaps.  The DDA's cells cover the parameter range [t0, T] it has walked without gaps (each cell's
+// entry is its predecessor's computed exit), and the exact ray point at any t of a cell's computed
+// interval lies within e <= 2^-19 (|o|_inf + B) of that cell (B: the grid's coordinate bound; binary32
+// origin, boundary and product roundings, approximate reciprocal), so any sphere hit at t' <= T in
+// binary64 is registered in a cell already walked when m >= e: build_grid sets m = 2^-12 (B + extent)
+// and grid_far = 2^7 (B + extent) bounds |o|_inf, so e <= 2^-12 (B + extent) (rays from farther away
+// test every sphere).  The walk stops when the best t is below the current cell's exit, so a sphere
+// reaching the best t exactly (a tie that World.hit's order decides) is still tested.  The closest hit
+// is therefore World.hit's, as for the BVH (tests/test_hostcheck.py, tests/test_gpu_parity.py).
+// RT_GRID_UNIFORM: cells that every active lane shares read through scalar loads — binary32 only (RTOW
+// 256 spp: f32 +0.6 %, f64 −0.8 %); 0 / 1: never / both precisions (A/B)
+#ifndef RT_GRID_UNIFORM
+#define RT_GRID_UNIFORM 2
+#endif
+template <class R>
+RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w) {
+    const R tmin = (R)0.001;
+    Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
+    brute_planes_boxes(sc, o, d, tmin, b);
+    float tl = bvh_tlimit(b.t);
+    const R a = dot(d, d);
+    FilterRay fr{};
+    if constexpr (sizeof(R) == 8) fr = make_filter_ray(o, d);
+    if (sc.num_big_spheres > 0) sphere_records(sc.big_spheres, 0, sc.num_big_spheres, o, d, a, fr, tmin, b, tl, w, true);
+    if (sc.num_grid_cells <= 0) return b;
+    const float of[3] = {(float)o.x, (float)o.y, (float)o.z};
+    const float df[3] = {(float)d.x, (float)d.y, (float)d.z};
+    if (!(fmaxf(fabsf(of[0]), fmaxf(fabsf(of[1]), fabsf(of[2]))) <= sc.grid_far)) {
+        // far origin (or NaN): every grid sphere once, in cell order (duplicates are harmless)
+        sphere_records(sc.grid_leaf, 0, sc.grid_cell[sc.num_grid_cells], o, d, a, fr, tmin, b, tl, w);
+        return b;
+    }
+    float inv[3], t0 = 0.0f, t1 = tl;
+    for (int k = 0; k < 3; ++k) {
+        float v = rt_rcp_approx(df[k]);
+        if (!(fabsf(v) <= 0x1p126f)) v = copysignf(0x1p126f, df[k]);
+        inv[k] = v;
+        const float ta = (sc.grid_lo[k] - of[k]) * v, tb = (sc.grid_hi[k] - of[k]) * v;
+        t0 = fmaxf(t0, fminf(ta, tb));
+        t1 = fminf(t1, fmaxf(ta, tb));
+    }
+    if (!(t0 <= t1)) return b;
+    int cell[3], step[3];
+    float tmax[3];
+    for (int k = 0; k < 3; ++k) {
+        const float p = of[k] + t0 * df[k];
+        int c = (int)floorf((p - sc.grid_lo[k]) / sc.grid_cs[k]);
+        c = c < 0 ? 0 : (c >= sc.grid_n[k] ? sc.grid_n[k] - 1 : c);
+        cell[k] = c;
+        step[k] = df[k] > 0.0f ? 1 : (df[k] < 0.0f ? -1 : 0);
+        tmax[k] = step[k] == 0 ? INFINITY
+                               : (sc.grid_lo[k] + (float)(c + (step[k] > 0)) * sc.grid_cs[k] - of[k]) * inv[k];
+    }
+    for (;;) {
+        RT_COUNT(++w.nodes);
+        const int ci = cell[0] + sc.grid_n[0] * (cell[1] + sc.grid_n[1] * cell[2]);
+#if RT_GRID_UNIFORM && defined(__HIP_DEVICE_COMPILE__)
+        // every active lane in one cell: its range and records through scalar loads
+        const int first = __builtin_amdgcn_readfirstlane(ci);
+        if ((RT_GRID_UNIFORM == 1 || sizeof(R) == 4) && __ballot(ci != first) == 0)
+            sphere_records(sc.grid_leaf, sc.grid_cell[first], sc.grid_cell[first + 1], o, d, a, fr, tmin, b, tl, w);
+        else
+#endif
+        sphere_records(sc.grid_leaf, sc.grid_cell[ci], sc.grid_cell[ci + 1], o, d, a, fr, tmin, b, tl, w);
+        const int ax = tmax[0] <= tmax[1] ? (tmax[0] <= tmax[2] ? 0 : 2) : (tmax[1] <= tmax[2] ? 1 : 2);
+        const float tx = tmax[ax];
+        // the best hit lies before this cell's exit; or the ray never leaves this cell at a finite t
+        // (zero / NaN direction; t beyond binary32's range is not modelled, as for the BVH)
+        if (b.t < (R)tx || !(tx < INFINITY)) break;
+        const int nc = cell[ax] + step[ax];
+        if (nc < 0 || nc >= sc.grid_n[ax]) break;
+        cell[ax] = nc;
+        tmax[ax] = (sc.grid_lo[ax] + (float)(nc + (step[ax] > 0)) * sc.grid_cs[ax] - of[ax]) * inv[ax];
+    }
+    return b;
+}
+
 // acceleration modes of the trace kernel
 // ACC_BVH_SPHERES: the ordered walk for scenes without triangles (sphere tree + planes/boxes only): the
 // kernel then holds no triangle-test code, and its binary64 form fits 5 waves/SIMD (RTOW +1.7 %)
 // ACC_BVH_SPHERES_LDS: the same walk with the sphere tree's nodes in LDS (trace_pool_lds_kernel)
-enum Accel : int { ACC_BRUTE = 0, ACC_BVH = 2, ACC_BVH_STACK = 3, ACC_BVH_SPHERES = 4, ACC_BVH_SPHERES_LDS = 5 };
+// ACC_GRID: sphere-only scenes through the uniform grid (closest_hit_grid)
+enum Accel : int { ACC_BRUTE = 0, ACC_BVH = 2, ACC_BVH_STACK = 3, ACC_BVH_SPHERES = 4, ACC_BVH_SPHERES_LDS = 5,
+                   ACC_GRID = 6 };
 
 template <class R, int ACC>
 RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
@@ -697,6 +789,7 @@ RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
     else if constexpr (ACC == ACC_BVH_STACK) return closest_hit_bvh<R, true>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_BVH_SPHERES) return closest_hit_bvh<R, true, false>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_BVH_SPHERES_LDS) return closest_hit_bvh<R, true, false, true>(sc, o, d, w, stk);
+    else if constexpr (ACC == ACC_GRID) return closest_hit_grid<R>(sc, o, d, w);
     else return closest_hit<R>(sc, o, d);
 }
 

@@ -64,8 +64,19 @@ constexpr bool dyn_stack() { return sizeof(R) == 4 || (RT_F64_DYN_STACK != 0 && 
 #define RT_LDS_OCC_F32 6
 #endif
 
+#ifndef RT_GRID_WAVES_PER_SIMD
+#define RT_GRID_WAVES_PER_SIMD 5
+#endif
+#ifndef RT_GRID_WAVES_F32
+#define RT_GRID_WAVES_F32 6
+#endif
+// walks with a per-lane LDS stack (the ordered BVH walks)
+template <int ACC>
+constexpr bool uses_stack() { return ACC == ACC_BVH_STACK || ACC == ACC_BVH_SPHERES || ACC == ACC_BVH_SPHERES_LDS; }
+
 template <class R, int ACC>
 constexpr int waves_per_simd() {
+    if constexpr (ACC == ACC_GRID) return sizeof(R) == 8 ? RT_GRID_WAVES_PER_SIMD : RT_GRID_WAVES_F32;
     if constexpr (ACC == ACC_BVH_SPHERES) return sizeof(R) == 8 ? RT_SPHERES_WAVES_PER_SIMD : RT_SPHERES_WAVES_F32;
     if constexpr (ACC == ACC_BVH_SPHERES_LDS) return sizeof(R) == 8 ? RT_LDS_OCC_F64 : RT_LDS_OCC_F32;
     return ACC >= ACC_BVH ? (sizeof(R) == 8 ? RT_BVH_WAVES_PER_SIMD : RT_BVH_WAVES_F32) : RT_MIN_WAVES_PER_SIMD;
@@ -114,7 +125,7 @@ __global__ __launch_bounds__(64, (waves_per_simd<R, ACC>()))
 void trace_kernel(const TraceArgs<R> args) {
     const ImageParams& im = args.im;
     BvhStack stk{nullptr, 0};
-    if constexpr (ACC >= ACC_BVH_STACK) {
+    if constexpr (uses_stack<ACC>()) {
         // per-lane traversal stacks, entry k of lane t at [k * 64 + t]: RT_BVH_STACK (binary64) or
         // sc.stack_entries (binary32: dynamic LDS sized by the launch to the scene's deepest leaf) x 4 B
         if constexpr (sizeof(R) == 8 && !dyn_stack<R, ACC>()) {
@@ -173,7 +184,7 @@ void trace_kernel(const TraceArgs<R> args) {
 #endif
 constexpr int kParkDoubles = 3, kParkInts = 6;
 template <class R, int ACC>
-constexpr bool parks() { return RT_PARK != 0 && sizeof(R) == 8 && ACC >= ACC_BVH_STACK; }
+constexpr bool parks() { return RT_PARK != 0 && sizeof(R) == 8 && uses_stack<ACC>(); }
 
 template <class R, bool COUNT, int ACC>
 __global__ __launch_bounds__(64, (waves_per_simd<R, ACC>()))
@@ -191,7 +202,7 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
         park_i = reinterpret_cast<uint32_t*>(park_dyn + kParkDoubles * 64) + threadIdx.x;
         stk.base = reinterpret_cast<int*>(park_dyn + kParkDoubles * 64) + kParkInts * 64 + threadIdx.x;
         stk.stride = 64;
-    } else if constexpr (ACC >= ACC_BVH_STACK) {
+    } else if constexpr (uses_stack<ACC>()) {
         // per-lane traversal stacks, entry k of lane t at [k * 64 + t]: RT_BVH_STACK (binary64) or
         // sc.stack_entries (binary32: dynamic LDS sized by the launch to the scene's deepest leaf) x 4 B
         if constexpr (sizeof(R) == 8 && !dyn_stack<R, ACC>()) {
@@ -538,7 +549,7 @@ static int pool_chunk(int ns, int tiles, bool tri_bvh) {
 // dynamic LDS of a trace launch: the ordered walk's per-lane stacks (the scene's deepest leaf entries)
 template <int ACC, class R>
 static size_t stack_lds_bytes(const SceneView<R>& sc) {
-    return ACC >= ACC_BVH_STACK && dyn_stack<R, ACC>() ? (size_t)std::min(sc.stack_entries, RT_BVH_STACK) * 64 * sizeof(int) : 0;
+    return uses_stack<ACC>() && dyn_stack<R, ACC>() ? (size_t)std::min(sc.stack_entries, RT_BVH_STACK) * 64 * sizeof(int) : 0;
 }
 // ... of the pool kernel (RT_PARK: the parked path state + the stack, binary64)
 template <int ACC, class R>
@@ -654,9 +665,14 @@ static int bvh_walk_mode(const SceneView<R>& sc) {
     static int v = -1;
     if (v == -1) {
         const char* e = getenv("RT_BVH_WALK");
-        v = e && !strncmp(e, "skip", 4) ? ACC_BVH : e && !strncmp(e, "two", 3) ? ACC_BVH_STACK : ACC_BVH_SPHERES;
+        // A/B: skip = stackless walk, two = the general ordered walk, tree = the sphere tree even where
+        // the grid was chosen, grid = the grid wherever one was built
+        v = e && !strncmp(e, "skip", 4) ? ACC_BVH : e && !strncmp(e, "two", 3) ? ACC_BVH_STACK
+          : e && !strncmp(e, "grid", 4) ? ACC_GRID : e && !strncmp(e, "tree", 4) ? -2 : ACC_BVH_SPHERES;
     }
-    return v == ACC_BVH_SPHERES && sc.num_tri_nodes > 0 ? ACC_BVH_STACK : v;
+    if (sc.num_tri_nodes > 0) return v == ACC_BVH ? ACC_BVH : ACC_BVH_STACK;
+    const bool grid = sc.num_grid_cells > 0 && (v == ACC_GRID || (v == ACC_BVH_SPHERES && sc.use_grid));
+    return grid ? ACC_GRID : v == -2 || v == ACC_GRID ? ACC_BVH_SPHERES : v;
 }
 
 template <class R, int ACC>
@@ -679,6 +695,7 @@ hipError_t launch_trace(const SceneView<R>& sc, const ImageParams& im, const Cou
     const int mode = bvh_walk_mode(sc);
     if (mode == ACC_BVH) return launch_acc<R, ACC_BVH>(a, count, pool, stream);
     if (mode == ACC_BVH_SPHERES) return launch_acc<R, ACC_BVH_SPHERES>(a, count, pool, stream);
+    if (mode == ACC_GRID) return launch_acc<R, ACC_GRID>(a, count, pool, stream);
     return launch_acc<R, ACC_BVH_STACK>(a, count, pool, stream);
 }
 
@@ -717,6 +734,7 @@ hipError_t launch_trace_partials(const SceneView<R>& sc, const ImageParams& im, 
     const int mode = bvh_walk_mode(sc);
     if (mode == ACC_BVH) return launch_partials_acc<R, ACC_BVH>(a, count, p, part, stream);
     if (mode == ACC_BVH_SPHERES) return launch_partials_acc<R, ACC_BVH_SPHERES>(a, count, p, part, stream);
+    if (mode == ACC_GRID) return launch_partials_acc<R, ACC_GRID>(a, count, p, part, stream);
     return launch_partials_acc<R, ACC_BVH_STACK>(a, count, p, part, stream);
 }
 
@@ -784,6 +802,8 @@ hipError_t launch_closest_hits(const SceneView<R>& sc, bool bvh, const double* r
         hipLaunchKernelGGL((closest_hits_lds_kernel<R>), grid, dim3(64), lb, stream, sc, rays, n, t, kind, idx);
     } else if (spheres)
         hipLaunchKernelGGL((closest_hits_kernel<R, ACC_BVH_SPHERES>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);
+    else if (bvh && bvh_walk_mode(sc) == ACC_GRID)
+        hipLaunchKernelGGL((closest_hits_kernel<R, ACC_GRID>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);
     else if (bvh) hipLaunchKernelGGL((closest_hits_kernel<R, ACC_BVH_STACK>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);
     else hipLaunchKernelGGL((closest_hits_kernel<R, ACC_BRUTE>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);
     return hipGetLastError();

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -25,6 +26,10 @@ struct HostScene {   // precision-independent staging, binary64 as packed by the
     std::vector<int> sphere_bvh_prims, tri_bvh_prims;
     std::vector<int> big_spheres;                                 // dominant spheres kept out of the tree
     std::vector<Bvh2Node> sphere_wide, tri_wide;                  // the same trees, two-child nodes
+    std::vector<int> grid_cell, grid_ids;                         // build_grid: cell offsets, sphere ids
+    int grid_n[3] = {0, 0, 0};
+    float grid_lo[3] = {0, 0, 0}, grid_hi[3] = {0, 0, 0}, grid_cs[3] = {1, 1, 1}, grid_far = 0;
+    bool use_grid = false;                                        // choose_walk(): the grid walks cheaper
     int bvh_depth = 0;                                            // deepest leaf of either tree
     int num_prims = 0;
     double record_bytes = 0;      // SURVEY §8d canonical bytes tested per segment
@@ -368,6 +373,103 @@ inline std::vector<int> peel_big_spheres(const HostScene& hs, std::vector<BuildP
     return big;
 }
 
+#ifndef RT_GRID_LAMBDA
+#define RT_GRID_LAMBDA 0.25       // cells per sphere (before rounding each axis up): RTOW 256 spp f64 / f32
+#endif                            // 0.0625 8667 / 11281, 0.125 8765 / 11497, 0.25 8817 / 11625, 0.35 8750 /
+                                  // 11577, 0.5 8718 / 11515, 1 8574 / 11346, 2 8135 / 10930, 4 7854 / 10515
+// Uniform grid over the spheres of the sphere tree (closest_hit_grid, pt_core.h): the box of those
+// spheres padded by m = 2^-12 (B + E) (B: largest |coordinate|, E: largest extent), ~RT_GRID_LAMBDA
+// cells per sphere of about cubic shape, every sphere registered in each cell its box padded by m
+// overlaps, in the cells' binary32 coordinates lo + k cs that the walk uses.  No grid when a sphere box
+// is not finite or the spheres are too few.
+inline void build_grid(HostScene& hs, const std::vector<BuildPrim>& prims) {
+    hs.grid_cell.clear();
+    hs.grid_ids.clear();
+    hs.grid_n[0] = hs.grid_n[1] = hs.grid_n[2] = 0;
+    if (prims.size() < 8) return;
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (const BuildPrim& p : prims)
+        for (int a = 0; a < 3; ++a) {
+            if (!std::isfinite(p.lo[a]) || !std::isfinite(p.hi[a])) return;
+            lo[a] = std::min(lo[a], p.lo[a]);
+            hi[a] = std::max(hi[a], p.hi[a]);
+        }
+    double B = 0, E = 0;
+    for (int a = 0; a < 3; ++a) {
+        B = std::max(B, std::max(std::fabs(lo[a]), std::fabs(hi[a])));
+        E = std::max(E, hi[a] - lo[a]);
+    }
+    if (!(B + E > 0) || !(B + E < 1e30)) return;
+    const double m = 0x1p-12 * (B + E);
+    double ext[3], vol = 1;
+    for (int a = 0; a < 3; ++a) {
+        lo[a] -= m;
+        hi[a] += m;
+        ext[a] = hi[a] - lo[a];
+        vol *= ext[a];
+    }
+    const double side = std::cbrt(vol / (RT_GRID_LAMBDA * (double)prims.size()));
+    long long total = 1;
+    for (int a = 0; a < 3; ++a) {
+        const double n = std::ceil(ext[a] / side);
+        hs.grid_n[a] = (int)std::min(256.0, std::max(1.0, n));
+        total *= hs.grid_n[a];
+        // binary32 cell geometry, rounded outward so that lo + n cs >= hi
+        float flo = (float)lo[a];
+        if ((double)flo > lo[a]) flo = std::nextafter(flo, -INFINITY);
+        float cs = (float)((hi[a] - (double)flo) / hs.grid_n[a]);
+        while ((double)flo + (double)hs.grid_n[a] * (double)cs < hi[a]) cs = std::nextafter(cs, INFINITY);
+        hs.grid_lo[a] = flo;
+        hs.grid_cs[a] = cs;
+        float fhi = (float)((double)flo + (double)hs.grid_n[a] * (double)cs);
+        if ((double)fhi < hi[a]) fhi = std::nextafter(fhi, INFINITY);
+        hs.grid_hi[a] = fhi;
+    }
+    hs.grid_far = (float)(0x1p6 * (B + E));
+    if (total > (1LL << 22)) { hs.grid_n[0] = hs.grid_n[1] = hs.grid_n[2] = 0; return; }
+    auto range = [&](const BuildPrim& p, int a, int& k0, int& k1) {
+        const double c = (double)hs.grid_cs[a], o = (double)hs.grid_lo[a];
+        k0 = (int)std::floor((p.lo[a] - m - o) / c);
+        k1 = (int)std::floor((p.hi[a] + m - o) / c);
+        k0 = std::max(0, std::min(hs.grid_n[a] - 1, k0));
+        k1 = std::max(0, std::min(hs.grid_n[a] - 1, k1));
+    };
+    long long regs = 0;           // registrations: give up on spheres too large for the cells
+    for (const BuildPrim& p : prims) {
+        long long r = 1;
+        for (int a = 0; a < 3; ++a) {
+            int k0, k1;
+            range(p, a, k0, k1);
+            r *= k1 - k0 + 1;
+        }
+        regs += r;
+    }
+    if (regs > 16LL * (long long)prims.size() + total) {
+        hs.grid_n[0] = hs.grid_n[1] = hs.grid_n[2] = 0;
+        return;
+    }
+    std::vector<int> count((size_t)total + 1, 0), cursor;
+    for (int pass = 0; pass < 2; ++pass) {
+        if (pass == 1) {            // count[c] -> offset of cell c; count[total] = registrations
+            for (size_t c = 1; c <= (size_t)total; ++c) count[c] += count[c - 1];
+            hs.grid_cell = count;
+            cursor.assign(count.begin(), count.end() - 1);
+            hs.grid_ids.assign((size_t)count[(size_t)total], 0);
+        }
+        for (const BuildPrim& p : prims) {
+            int k0[3], k1[3];
+            for (int a = 0; a < 3; ++a) range(p, a, k0[a], k1[a]);
+            for (int z = k0[2]; z <= k1[2]; ++z)
+                for (int y = k0[1]; y <= k1[1]; ++y)
+                    for (int x = k0[0]; x <= k1[0]; ++x) {
+                        const size_t c = (size_t)x + (size_t)hs.grid_n[0] * ((size_t)y + (size_t)hs.grid_n[1] * z);
+                        if (pass == 0) ++count[c + 1];
+                        else hs.grid_ids[(size_t)cursor[c]++] = p.idx;
+                    }
+        }
+    }
+}
+
 inline void build_bvhs(HostScene& hs) {
     BvhBuilder sb;
     sb.kLeafMax = RT_BVH_SPHERE_LEAF;
@@ -381,6 +483,7 @@ inline void build_bvhs(HostScene& hs) {
         sb.prims.push_back(p);
     }
     hs.big_spheres = peel_big_spheres(hs, sb.prims);
+    build_grid(hs, sb.prims);
     if (!sb.prims.empty()) sb.build(0, (int)sb.prims.size());
     hs.bvh_depth = sb.max_depth;
     hs.sphere_bvh = std::move(sb.nodes);
@@ -422,6 +525,7 @@ struct HostRecords {
     std::vector<SphereLeaf<R>> bvh_sphere_leaf;
     std::vector<TriLeaf<R>> bvh_tri_leaf;
     std::vector<SphereLeaf<R>> big_sphere_leaf;   // HostScene::big_spheres, tested before the walk
+    std::vector<SphereLeaf<R>> grid_leaf;         // HostScene::grid_ids, cell by cell
 };
 
 template <class R>
@@ -479,6 +583,7 @@ void make_records(const HostScene& hs, const rt_scene_desc& d, HostRecords<R>& o
     };
     for (int id : hs.sphere_bvh_prims) out.bvh_sphere_leaf.push_back(leaf(id));
     for (int id : hs.big_spheres) out.big_sphere_leaf.push_back(leaf(id));
+    for (int id : hs.grid_ids) out.grid_leaf.push_back(leaf(id));
     for (int id : hs.tri_bvh_prims) {
         const TriRec<R>& r = out.tris[id];
         out.bvh_tri_leaf.push_back(TriLeaf<R>{{r.v0x, r.v0y, r.v0z, r.e1x, r.e1y, r.e1z, r.e2x, r.e2y, r.e2z},
@@ -499,6 +604,15 @@ void fill_view_constants(SceneView<R>& v, const HostScene& hs, const rt_scene_de
     v.num_sphere_wide = (int)hs.sphere_wide.size();
     v.num_tri_wide = (int)hs.tri_wide.size();
     v.num_big_spheres = (int)hs.big_spheres.size();
+    v.num_grid_cells = hs.grid_n[0] * hs.grid_n[1] * hs.grid_n[2];
+    for (int k = 0; k < 3; ++k) {
+        v.grid_n[k] = hs.grid_n[k];
+        v.grid_lo[k] = hs.grid_lo[k];
+        v.grid_hi[k] = hs.grid_hi[k];
+        v.grid_cs[k] = hs.grid_cs[k];
+    }
+    v.grid_far = hs.grid_far;
+    v.use_grid = hs.use_grid ? 1 : 0;
     v.stack_entries = std::max(1, hs.bvh_depth);
     const rt_camera_desc& c = d.camera;
     for (int k = 0; k < 3; ++k) {
@@ -521,6 +635,61 @@ inline uint32_t host_seed_mix(uint32_t seed) {
     uint32_t x = seed ^ 0x3C6EF372U;
     x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
     return x;
+}
+
+// Walk choice for a sphere-only scene with a grid: the BVH and the grid walk give the same closest hit,
+// so the choice is about speed only.  Both host walks (the kernel's own code) run over a sample of the
+// scene's rays — a 48 x 27 raster of pixel-centre camera rays and, from each hit, one ray in a random
+// direction — and the grid is chosen when its estimated cost (cells + 0.5 per sphere test) is below
+// 0.8 x the tree's (nodes + 0.5 per sphere test); RTOW: ~3.9 vs ~8.0.
+#ifndef RT_GRID_CHOICE
+#define RT_GRID_CHOICE 0.8
+#endif
+inline void choose_walk(HostScene& hs, const rt_scene_desc& d) {
+    hs.use_grid = false;
+    if (hs.grid_n[0] * hs.grid_n[1] * hs.grid_n[2] <= 0 || !hs.tri_mat.empty() || hs.bvh_depth > 64) return;
+    HostRecords<double> rec;
+    make_records(hs, d, rec);
+    SceneView<double> v{};
+    v.runs = hs.runs.data();
+    v.spheres = rec.spheres.data(); v.sphere_filter = rec.sphere_filter.data(); v.sphere_r = rec.sphere_r.data();
+    v.planes = rec.planes.data(); v.boxes = rec.boxes.data(); v.tris = rec.tris.data();
+    v.sphere_mat = hs.sphere_mat.data(); v.plane_mat = hs.plane_mat.data(); v.box_mat = hs.box_mat.data();
+    v.tri_mat = hs.tri_mat.data(); v.mats = rec.mats.data(); v.perm = rec.perm.data();
+    v.plane_obj = hs.plane_obj.data(); v.box_obj = hs.box_obj.data();
+    v.sphere_nodes = hs.sphere_bvh.data(); v.tri_nodes = hs.tri_bvh.data();
+    v.bvh_sphere_leaf = rec.bvh_sphere_leaf.data(); v.bvh_tri_leaf = rec.bvh_tri_leaf.data();
+    v.big_spheres = rec.big_sphere_leaf.data();
+    v.sphere_wide = hs.sphere_wide.data(); v.tri_wide = hs.tri_wide.data();
+    v.grid_cell = hs.grid_cell.data(); v.grid_leaf = rec.grid_leaf.data();
+    fill_view_constants(v, hs, d);
+    const rt_camera_desc& c = d.camera;
+    int stack[64];
+    double tree = 0, grid = 0;
+    uint32_t rng = 0x9e3779b9u;
+    auto uni = [&]() { rng = rng * 1664525u + 1013904223u; return (double)(rng >> 8) * 0x1p-24 * 2.0 - 1.0; };
+    for (int j = 0; j < 27; ++j)
+        for (int i = 0; i < 48; ++i) {
+            const double u = (i + 0.5) / 48, w = (j + 0.5) / 27;
+            V3<double> o{c.origin[0], c.origin[1], c.origin[2]};
+            V3<double> dir{c.lower_left[0] + u * c.horizontal[0] + w * c.vertical[0] - o.x,
+                           c.lower_left[1] + u * c.horizontal[1] + w * c.vertical[1] - o.y,
+                           c.lower_left[2] + u * c.horizontal[2] + w * c.vertical[2] - o.z};
+            for (int bounce = 0; bounce < 2; ++bounce) {
+                Work wt{}, wg{};
+                const Closest<double> h = closest_hit_bvh<double, true, false>(v, o, dir, wt, BvhStack{stack, 1});
+                closest_hit_grid<double>(v, o, dir, wg);
+                tree += wt.nodes + 0.5 * wt.spheres;
+                grid += wg.nodes + 0.5 * wg.spheres;
+                if (h.kind == HIT_NONE) break;
+                o = o + dir * h.t;
+                dir = V3<double>{uni(), uni(), uni()};
+            }
+        }
+    hs.use_grid = grid < RT_GRID_CHOICE * tree;
+    if (getenv("RT_WALK_DEBUG"))
+        fprintf(stderr, "[rt] walk choice: tree %.3g, grid %.3g (%d x %d x %d cells) -> %s\n", tree, grid, hs.grid_n[0],
+                hs.grid_n[1], hs.grid_n[2], hs.use_grid ? "grid" : "tree");
 }
 
 }  // namespace rt

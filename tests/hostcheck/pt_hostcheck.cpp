@@ -19,6 +19,7 @@ struct HostView {
         std::string err;
         if (!pack_host(*d, hs, err)) return false;
         build_bvhs(hs);
+        choose_walk(hs, *d);
         make_records(hs, *d, rec);
         v.runs = hs.runs.data();
         v.spheres = rec.spheres.data(); v.sphere_filter = rec.sphere_filter.data(); v.sphere_r = rec.sphere_r.data(); v.planes = rec.planes.data();
@@ -30,6 +31,7 @@ struct HostView {
         v.bvh_sphere_leaf = rec.bvh_sphere_leaf.data(); v.bvh_tri_leaf = rec.bvh_tri_leaf.data();
         v.big_spheres = rec.big_sphere_leaf.data();
         v.sphere_wide = hs.sphere_wide.data(); v.tri_wide = hs.tri_wide.data();
+        v.grid_cell = hs.grid_cell.data(); v.grid_leaf = rec.grid_leaf.data();
         fill_view_constants(v, hs, *d);
         return hs.bvh_depth <= 64;                   // the host walks use 64-entry stacks
     }
@@ -63,6 +65,7 @@ static int render(const rt_scene_desc* d, const rt_settings* s, double* sum, uin
             if (im.max_depth > 0)
                 r = s->accel == RT_ACCEL_BVH ? trace_pixel<R, true, ACC_BVH_STACK>(v, im, cx, cy, im.s_end, acc, stk)
                   : s->accel == 3            ? trace_pixel<R, true, ACC_BVH>(v, im, cx, cy, im.s_end, acc)
+                  : s->accel == 4            ? trace_pixel<R, true, ACC_GRID>(v, im, cx, cy, im.s_end, acc)
                                              : trace_pixel<R, true, ACC_BRUTE>(v, im, cx, cy, im.s_end, acc);
             segs[q] = r.segments;
             draws[q] = r.draws;
@@ -255,8 +258,10 @@ extern "C" long long ptc_bvh_check(const rt_scene_desc* d, long long n, unsigned
         int stack[RT_BVH_STACK];
         const Closest<double> b = closest_hit_bvh<double, false>(v, O, D, w, BvhStack{nullptr, 0});
         const Closest<double> c = closest_hit_bvh<double, true>(v, O, D, w, BvhStack{stack, 1});
+        const Closest<double> g = v.num_grid_cells > 0 && v.num_tri_nodes == 0
+                                      ? closest_hit_grid<double>(v, O, D, w) : c;
         if (a.kind != HIT_NONE) ++nh;
-        for (const Closest<double>& x : {b, c}) {
+        for (const Closest<double>& x : {b, c, g}) {
             const bool same = a.kind == x.kind && (a.kind == HIT_NONE || (a.idx == x.idx && a.mat == x.mat &&
                                                                          std::memcmp(&a.t, &x.t, 8) == 0));
             bad += !same;
@@ -278,8 +283,8 @@ extern "C" int ptc_bvh_info(const rt_scene_desc* d, int* depth, int* nodes2, int
     return 0;
 }
 
-// Work totals of the two-child walk over a crop (host experiments on BVH quality, TEST/DEV TOOL):
-// out = {segments, nodes, sphere tests, triangle tests}
+// Work totals of the two-child walk (s->accel != 4) or the grid walk (4) over a crop (host experiments
+// on BVH quality, TEST/DEV TOOL): out = {segments, nodes or cells, sphere tests, triangle tests}
 extern "C" int ptc_work(const rt_scene_desc* d, const rt_settings* s, double* out) {
     HostView<double> hv;
     if (!hv.init(d)) return -1;
@@ -300,7 +305,8 @@ extern "C" int ptc_work(const rt_scene_desc* d, const rt_settings* s, double* ou
     for (int cy = 0; cy < im.ch; ++cy)
         for (int cx = 0; cx < im.cw; ++cx) {
             double acc[3] = {0, 0, 0};
-            const PixelResult r = trace_pixel<double, true, ACC_BVH_STACK>(hv.v, im, cx, cy, im.s_end, acc, stk);
+            const PixelResult r = s->accel == 4 ? trace_pixel<double, true, ACC_GRID>(hv.v, im, cx, cy, im.s_end, acc)
+                                                : trace_pixel<double, true, ACC_BVH_STACK>(hv.v, im, cx, cy, im.s_end, acc, stk);
             out[0] += r.segments; out[1] += r.work.nodes; out[2] += r.work.spheres; out[3] += r.work.tris;
         }
     return 0;

@@ -289,10 +289,11 @@ def _render_in_child(script, path, **env):
     return np.load(path)
 
 
-@pytest.mark.parametrize("walk", ["skip"])
+@pytest.mark.parametrize("walk", ["skip", "tree", "grid"])
 def test_alternative_bvh_walks_bit_identical(gpu, tmp_path, walk):
-    """The A/B walk (RT_BVH_WALK=skip: stackless preorder) renders the same bits as the default
-    two-child walk (run in child processes: the walk is chosen per process)."""
+    """Every walk renders the same bits as the general two-child walk (RT_BVH_WALK=two): skip = the
+    stackless preorder walk, tree = the sphere tree where the uniform grid was chosen (RTOW), grid =
+    the grid wherever one was built (run in child processes: the walk is chosen per process)."""
     res = {mode: _render_in_child(_WALK_SCRIPT, tmp_path / f"{mode}.npz", RT_BVH_WALK=mode) for mode in ("two", walk)}
     for k in res["two"].files:
         assert np.array_equal(res["two"][k], res[walk][k], equal_nan=True), k
@@ -546,6 +547,35 @@ def test_multi_device_distinct_gpus(gpu):
         assert np.array_equal(one[k], many[k]), k
     assert np.allclose(one["mean"], many["mean"], rtol=SUM_RTOL, atol=0)
     rt.close()
+
+
+_TREE_PROOF_SCRIPT = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + "/tests")
+import torch  # noqa: F401  (HIP runtime first)
+import hostcheck_binding as hb
+from blenderraytracer_amd import capi
+from blenderraytracer_amd.renderer import GpuRayTracer
+from blenderraytracer_amd.scene import load_scene_json
+from test_gpu_parity import _closest_hits
+rt = GpuRayTracer(64, 36, seed=3)
+assert rt.load_from_json(load_scene_json("rtow.json"))
+r, ht, hk, hi = hb.bvh_rays(rt.packed(), 200000, 99, 0)
+bt, bk, bi = _closest_hits(rt, r, capi.RT_PREC_F64, capi.RT_ACCEL_BRUTE)
+vt, vk, vi = _closest_hits(rt, r, capi.RT_PREC_F64, capi.RT_ACCEL_BVH)
+np.savez(sys.argv[2], bt=bt, bk=bk, bi=bi, vt=vt, vk=vk, vi=vi)
+'''
+
+
+@pytest.mark.parametrize("walk", ["tree", "grid"])
+def test_rtow_walks_closest_hit_identical_on_device(gpu, tmp_path, walk):
+    """RTOW's two sphere walks, each forced in a child process (the trace kernel uses the grid there),
+    on the host check's 200k adversarial rays through rt_closest_hits: device walk == device World
+    order, bit for bit (t, kind, index)."""
+    res = _render_in_child(_TREE_PROOF_SCRIPT, tmp_path / f"{walk}.npz", RT_BVH_WALK=walk)
+    assert (res["bk"] >= 0).sum() > len(res["bk"]) // 10
+    assert np.array_equal(res["bk"], res["vk"]) and np.array_equal(res["bi"], res["vi"])
+    assert np.array_equal(res["bt"].view(np.uint64), res["vt"].view(np.uint64))
 
 
 def _closest_hits(rt, rays, precision, accel):
