@@ -389,6 +389,11 @@ def main():
         else:
             flops = seg_launch * flops_per_segment
         rank_samples = cfg["w"] * cfg["h"] * (job.range[1] - job.range[0])
+        # the walk this render ran (rt_scene_walk): BVH nodes or grid cells are its walk steps
+        walk = {0: "world_order", 1: "bvh", 2: "uniform_grid"}.get(
+            capi.load_library().rt_scene_walk(rt.scene_handle(), capi.RT_PREC_F32 if args.precision == "f32" else capi.RT_PREC_F64,
+                                              {"auto": capi.RT_ACCEL_AUTO, "brute": capi.RT_ACCEL_BRUTE, "bvh": capi.RT_ACCEL_BVH}[args.accel]),
+            "error")
         kernel_desc = ("trace step: trace_pool_kernel (trace_pool_lds_kernel for binary32 sphere scenes) + "
                        "reduce_kernel (one launch each per frame)")
         roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
@@ -451,12 +456,14 @@ def main():
         roofline.update({
             "cache_served_bytes": a_bytes,
             "cache_served_GBps": round(a_bytes / (k_ms * 1e-3) / 1e9, 2),
-            "cache_served_definition": ("SURVEY 8d algorithmic bytes, BVH form: 64 B/node visited + 16 B/sphere + "
-                                        "36 B/triangle tested + segments x 24 B/plane|box + 12 B/pixel; read from "
-                                        "L1/L2 (the trees are cache-resident), not HBM" if bvh else
+            "cache_served_definition": ("SURVEY 8d algorithmic bytes, BVH form: 64 B/node visited (8 B/cell for the "
+                                        "uniform-grid walk) + 16 B/sphere + 36 B/triangle tested + segments x 24 "
+                                        "B/plane|box + 12 B/pixel; read from L1/L2 (the trees are cache-resident), "
+                                        "not HBM" if bvh else
                                         "SURVEY 8d algorithmic bytes: segments x sum(prim record bytes: sphere 16, "
                                         "plane 24, box 24, tri 36) + 12 B/pixel; scalar (SGPR) loads, not HBM"),
-            "bvh_nodes_per_segment": round(nodes / seg_launch, 3) if bvh else None,
+            "walk": walk,
+            "walk_steps_per_segment": round(nodes / seg_launch, 3) if bvh else None,
             "prim_tests_per_segment": round((sph + tri) / seg_launch, 3) if bvh else None})
         if world > 1:
             mp_mode = {"mode": "ranks", "world_size": dist.get_world_size(), "backend": dist.get_backend(),

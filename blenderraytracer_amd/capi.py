@@ -92,6 +92,7 @@ EXPORTS = {
     "rt_cancel": (C.c_int, [C.c_void_p]),
     "rt_closest_hits": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_double), C.c_size_t,
                                   C.POINTER(C.c_double), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "rt_scene_walk": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "rt_render_checkpoint": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_size_t, C.POINTER(C.c_int32)]),
     "rt_render_resume": (C.c_int, [C.c_void_p, C.POINTER(Settings), C.POINTER(C.c_double), C.c_int32,
                                    C.POINTER(Output), PROGRESS_FN, C.c_void_p, C.POINTER(Stats)]),

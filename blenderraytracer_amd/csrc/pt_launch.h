@@ -50,6 +50,9 @@ hipError_t launch_closest_hits(const SceneView<R>& sc, bool bvh, const double* r
 // default of rt_settings.sum_order = RT_SUM_POOL: the sample pool, unless RT_SAMPLE_POOL=0 is set in the
 // environment (A/B runs of the lane-per-pixel kernel)
 bool trace_uses_pool();
+// the BVH-mode trace of this scene walks the uniform grid (ACC_GRID) rather than a tree
+template <class R>
+bool trace_walks_grid(const SceneView<R>& sc);
 // scratch bytes the sample pool needs to trace `ns` samples of a cw x ch crop in one launch (0: one
 // chunk, the partials go straight to the sums).  With less scratch (but at least one chunk's worth,
 // tiles x kPartialBytesPerTile) launch_trace splits the samples over several launches.

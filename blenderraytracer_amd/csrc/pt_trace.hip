@@ -675,6 +675,11 @@ static int bvh_walk_mode(const SceneView<R>& sc) {
     return grid ? ACC_GRID : v == -2 || v == ACC_GRID ? ACC_BVH_SPHERES : v;
 }
 
+template <class R>
+bool trace_walks_grid(const SceneView<R>& sc) { return bvh_walk_mode(sc) == ACC_GRID; }
+template bool trace_walks_grid<double>(const SceneView<double>&);
+template bool trace_walks_grid<float>(const SceneView<float>&);
+
 template <class R, int ACC>
 static hipError_t launch_acc(const TraceArgs<R>& a, bool count, bool pool, hipStream_t stream) {
     if (pool) return launch_pool<R, ACC>(a, count, stream);

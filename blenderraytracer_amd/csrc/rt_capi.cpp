@@ -482,8 +482,11 @@ void fill_stats(rt_stats* st, const rt_scene* sc, const rt_settings* s, const un
         st->sphere_tests = totals[2];
         st->tri_tests = totals[3];
         st->prim_tests = totals[2] + totals[3] + totals[0] * brute;
-        st->algorithmic_bytes = 64.0 * totals[1] + 16.0 * totals[2] + 36.0 * totals[3] + 24.0 * totals[0] * brute +
-                                12.0 * (double)n;
+        // a walk step reads a 64-B two-child node, or a grid cell's 8-B record range (node_visits then
+        // counts cells)
+        const bool grid = s->precision == RT_PREC_F32 ? trace_walks_grid(sc->home.s32.view) : trace_walks_grid(sc->home.s64.view);
+        st->algorithmic_bytes = (grid ? 8.0 : 64.0) * totals[1] + 16.0 * totals[2] + 36.0 * totals[3] +
+                                24.0 * totals[0] * brute + 12.0 * (double)n;
     } else {
         st->node_visits = st->sphere_tests = st->tri_tests = 0;
         st->prim_tests = totals[0] * (uint64_t)sc->num_prims;
@@ -998,6 +1001,19 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
         }
     }
     return RT_OK;
+}
+
+int rt_scene_walk(rt_scene* sc, int32_t precision, int32_t accel) {
+    if (!sc) return fail(RT_ERR_INVALID, "NULL argument");
+    if (precision != RT_PREC_F64 && precision != RT_PREC_F32) return fail(RT_ERR_INVALID, "precision %d", precision);
+    rt_settings s{};
+    s.accel = accel;
+    if (s.accel < RT_ACCEL_AUTO || s.accel > RT_ACCEL_BVH) return fail(RT_ERR_INVALID, "accel %d", accel);
+    const int rc = check_accel(sc, &s);
+    if (rc) return rc;
+    if (!use_bvh(sc, &s)) return 0;
+    const bool grid = precision == RT_PREC_F32 ? trace_walks_grid(sc->home.s32.view) : trace_walks_grid(sc->home.s64.view);
+    return grid ? 2 : 1;
 }
 
 int rt_closest_hits(rt_scene* sc, int32_t precision, int32_t accel, const double* rays, size_t n, double* t,

@@ -268,6 +268,12 @@ int rt_finalize_device(rt_scene* scene, const rt_settings* settings, const doubl
 int rt_closest_hits(rt_scene* scene, int32_t precision, int32_t accel, const double* rays, size_t n,
                     double* t, int32_t* kind, int32_t* index);
 
+/* Diagnostic: the walk a render with these precision / accel settings runs on this scene — 0 World.objects
+ * order (brute force), 1 a BVH tree walk, 2 the uniform grid over the spheres (sphere-only scenes where
+ * the host's sampled cost estimate prefers it, scene_pack.h choose_walk); < 0 an error status.  Every
+ * walk finds the same closest hit; they differ in speed only. */
+int rt_scene_walk(rt_scene* scene, int32_t precision, int32_t accel);
+
 /* Request cancellation of an in-flight rt_render on `scene` (polled between sample batches). */
 int rt_cancel(rt_scene* scene);
 
