@@ -317,3 +317,13 @@ extern "C" void ptc_pow5(const double* x, double* out, long long n) {
     for (long long i = 0; i < n; ++i) out[i] = rt::pow5_rn<double>(x[i]);
 }
 
+
+// Grid shape (build_grid): cells per axis and sphere registrations (TEST/DEV TOOL)
+extern "C" int ptc_grid_info(const rt_scene_desc* d, int* n3, long long* regs, int* use_grid) {
+    HostView<double> hv;
+    hv.init(d);
+    for (int k = 0; k < 3; ++k) n3[k] = hv.hs.grid_n[k];
+    *regs = (long long)hv.hs.grid_ids.size();
+    *use_grid = hv.hs.use_grid ? 1 : 0;
+    return 0;
+}
