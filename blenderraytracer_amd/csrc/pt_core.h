@@ -156,6 +156,7 @@ struct SceneView {
     float grid_lo[3], grid_hi[3], grid_cs[3];   // cells [lo + k cs, lo + (k+1) cs); hi: the padded box
     float grid_far;                // rays with |origin|_inf beyond this take the sphere-list fallback
     int num_grid_cells;            // 0: no grid
+    int num_grid_recs;             // grid_cell[num_grid_cells]: registrations (records in grid_leaf)
     int use_grid;                  // choose_walk (scene_pack.h): the trace kernel walks the grid
     // camera (camera.js:8-36 vectors, computed on the host in binary64)
     R cam_o[3], cam_llc[3], cam_h[3], cam_v[3], cam_u[3], cam_vv[3], cam_w[3];
@@ -449,7 +450,13 @@ typedef unsigned int rt_u4 __attribute__((ext_vector_type(4)));
 // GPU, strided by the workgroup size so a wave's accesses are conflict-free).  box / kid: the sphere
 // tree's nodes copied to LDS (ACC_BVH_SPHERES_LDS): node i's child boxes at box[3i .. 3i+2], its child
 // references at kid[i]
-struct BvhStack { int* base; int stride; const rt_u4* box = nullptr; const rt_u2* kid = nullptr; };
+// gcell / grec: the grid's cell offsets and records copied to LDS (ACC_GRID_LDS): binary64 keeps the
+// 16-B binary32 filters there (the rest of a record is read from grid_leaf by filter survivors only),
+// binary32 the whole 32-B records (grec[2k], grec[2k + 1])
+struct BvhStack {
+    int* base; int stride; const rt_u4* box = nullptr; const rt_u2* kid = nullptr;
+    const int* gcell = nullptr; const rt_u4* grec = nullptr;
+};
 
 #if defined(__HIP_DEVICE_COMPILE__)
 // IEEE 754-2019 minimum / maximum (v_minimum3_f32 / v_maximum3_f32 on gfx950): unlike fminf / fmaxf
@@ -712,8 +719,58 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
 #ifndef RT_GRID_UNIFORM
 #define RT_GRID_UNIFORM 2
 #endif
+// Grid records [first, end) read from their LDS copy (ACC_GRID_LDS): binary64 tests the binary32 filter
+// from LDS and reads the rest of the record from recs only when it passes; binary32 reads the whole
+// record from LDS.  The same tests in the same order as sphere_records: same hits, same bits.
 template <class R>
-RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w) {
+RT_HD void sphere_records_lds(const rt_u4* lrec, const SphereLeaf<R>* recs, int first, int end, V3<R> o, V3<R> d,
+                              R a, const FilterRay& fr, R tmin, Closest<R>& b, float& tl, Work& w) {
+    RT_COUNT(w.spheres += end - first);
+    for (int k = first; k < end; ++k) {
+        SphereRec<R> s;
+        int id, obj, mat;
+        if constexpr (sizeof(R) == 8) {
+            const rt_u4 q = lrec[k];
+            SphereFilter f;
+            memcpy(&f, &q, sizeof f);
+            if (!sphere_filter_pass(f, fr)) continue;
+            s = recs[k].s;
+            id = recs[k].id; obj = recs[k].obj; mat = recs[k].mat;
+        } else {
+            const rt_u4 q0 = lrec[2 * k], q1 = lrec[2 * k + 1];
+            memcpy(&s, &q0, sizeof s);
+            id = (int)q1.x; obj = (int)q1.y; mat = (int)q1.z;
+        }
+        R t;
+        if (!sphere_candidate(s, o, d, a, tmin, t)) continue;
+        if (better(t, obj, id, b)) {
+            b = Closest<R>{t, HIT_SPHERE, id, mat, obj};
+            tl = bvh_tlimit(b.t);
+        }
+    }
+}
+
+// The grid's LDS copy (ACC_GRID_LDS): record k's binary32 filter (binary64) or whole record (binary32)
+// at grec, the cell offsets at gcell; lanes t, t + threads, ... of a workgroup copy their share
+template <class R>
+RT_HD size_t grid_lds_rec_bytes(const SceneView<R>& sc) { return (size_t)sc.num_grid_recs * (sizeof(R) == 8 ? 16 : 32); }
+template <class R>
+RT_HD size_t grid_lds_bytes(const SceneView<R>& sc) {
+    return grid_lds_rec_bytes(sc) + 4 * (size_t)(sc.num_grid_cells + 1);
+}
+template <class R>
+RT_HD void copy_grid_lds(const SceneView<R>& sc, rt_u4* grec, int* gcell, int t, int threads) {
+    const rt_u4* g = reinterpret_cast<const rt_u4*>(sc.grid_leaf);
+    for (int k = t; k < sc.num_grid_recs; k += threads) {
+        if constexpr (sizeof(R) == 8) grec[k] = g[4 * k];               // the 16-B filter of a 64-B record
+        else { grec[2 * k] = g[2 * k]; grec[2 * k + 1] = g[2 * k + 1]; }
+    }
+    for (int k = t; k <= sc.num_grid_cells; k += threads) gcell[k] = sc.grid_cell[k];
+}
+
+// LDSG: the cell offsets and records come from their LDS copy in stk (ACC_GRID_LDS)
+template <class R, bool LDSG = false>
+RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, const BvhStack& stk) {
     const R tmin = (R)0.001;
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
     brute_planes_boxes(sc, o, d, tmin, b);
@@ -754,6 +811,9 @@ RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work
     for (;;) {
         RT_COUNT(++w.nodes);
         const int ci = cell[0] + sc.grid_n[0] * (cell[1] + sc.grid_n[1] * cell[2]);
+        if constexpr (LDSG) {
+            sphere_records_lds(stk.grec, sc.grid_leaf, stk.gcell[ci], stk.gcell[ci + 1], o, d, a, fr, tmin, b, tl, w);
+        } else {
 #if RT_GRID_UNIFORM && defined(__HIP_DEVICE_COMPILE__)
         // every active lane in one cell: its range and records through scalar loads
         const int first = __builtin_amdgcn_readfirstlane(ci);
@@ -762,6 +822,7 @@ RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work
         else
 #endif
         sphere_records(sc.grid_leaf, sc.grid_cell[ci], sc.grid_cell[ci + 1], o, d, a, fr, tmin, b, tl, w);
+        }
         const int ax = tmax[0] <= tmax[1] ? (tmax[0] <= tmax[2] ? 0 : 2) : (tmax[1] <= tmax[2] ? 1 : 2);
         const float tx = tmax[ax];
         // the best hit lies before this cell's exit; or the ray never leaves this cell at a finite t
@@ -780,8 +841,9 @@ RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work
 // kernel then holds no triangle-test code, and its binary64 form fits 5 waves/SIMD (RTOW +1.7 %)
 // ACC_BVH_SPHERES_LDS: the same walk with the sphere tree's nodes in LDS (trace_pool_lds_kernel)
 // ACC_GRID: sphere-only scenes through the uniform grid (closest_hit_grid)
+// ACC_GRID_LDS: the same walk with the grid's cell offsets and records (binary64: their filters) in LDS
 enum Accel : int { ACC_BRUTE = 0, ACC_BVH = 2, ACC_BVH_STACK = 3, ACC_BVH_SPHERES = 4, ACC_BVH_SPHERES_LDS = 5,
-                   ACC_GRID = 6 };
+                   ACC_GRID = 6, ACC_GRID_LDS = 7 };
 
 template <class R, int ACC>
 RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
@@ -789,7 +851,8 @@ RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
     else if constexpr (ACC == ACC_BVH_STACK) return closest_hit_bvh<R, true>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_BVH_SPHERES) return closest_hit_bvh<R, true, false>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_BVH_SPHERES_LDS) return closest_hit_bvh<R, true, false, true>(sc, o, d, w, stk);
-    else if constexpr (ACC == ACC_GRID) return closest_hit_grid<R>(sc, o, d, w);
+    else if constexpr (ACC == ACC_GRID) return closest_hit_grid<R>(sc, o, d, w, stk);
+    else if constexpr (ACC == ACC_GRID_LDS) return closest_hit_grid<R, true>(sc, o, d, w, stk);
     else return closest_hit<R>(sc, o, d);
 }
 

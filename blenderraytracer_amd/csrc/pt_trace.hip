@@ -76,7 +76,7 @@ constexpr bool uses_stack() { return ACC == ACC_BVH_STACK || ACC == ACC_BVH_SPHE
 
 template <class R, int ACC>
 constexpr int waves_per_simd() {
-    if constexpr (ACC == ACC_GRID) return sizeof(R) == 8 ? RT_GRID_WAVES_PER_SIMD : RT_GRID_WAVES_F32;
+    if constexpr (ACC == ACC_GRID || ACC == ACC_GRID_LDS) return sizeof(R) == 8 ? RT_GRID_WAVES_PER_SIMD : RT_GRID_WAVES_F32;
     if constexpr (ACC == ACC_BVH_SPHERES) return sizeof(R) == 8 ? RT_SPHERES_WAVES_PER_SIMD : RT_SPHERES_WAVES_F32;
     if constexpr (ACC == ACC_BVH_SPHERES_LDS) return sizeof(R) == 8 ? RT_LDS_OCC_F64 : RT_LDS_OCC_F32;
     return ACC >= ACC_BVH ? (sizeof(R) == 8 ? RT_BVH_WAVES_PER_SIMD : RT_BVH_WAVES_F32) : RT_MIN_WAVES_PER_SIMD;
@@ -433,8 +433,18 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
 #ifndef RT_LDS_WAVES_F32
 #define RT_LDS_WAVES_F32 12       // 2 workgroups per CU at 6 waves/SIMD
 #endif
-template <class R>
-constexpr int lds_waves() { return sizeof(R) == 8 ? RT_LDS_WAVES_F64 : RT_LDS_WAVES_F32; }
+// the grid's LDS kernel (ACC_GRID_LDS) holds no stacks: smaller workgroups, each with its own copy
+#ifndef RT_GRID_LDS_WAVES_F64
+#define RT_GRID_LDS_WAVES_F64 4   // 5 workgroups per CU at 5 waves/SIMD
+#endif
+#ifndef RT_GRID_LDS_WAVES_F32
+#define RT_GRID_LDS_WAVES_F32 8   // 3 workgroups per CU at 6 waves/SIMD
+#endif
+template <class R, int ACC = ACC_BVH_SPHERES_LDS>
+constexpr int lds_waves() {
+    if constexpr (ACC == ACC_GRID_LDS) return sizeof(R) == 8 ? RT_GRID_LDS_WAVES_F64 : RT_GRID_LDS_WAVES_F32;
+    return sizeof(R) == 8 ? RT_LDS_WAVES_F64 : RT_LDS_WAVES_F32;
+}
 constexpr int kPoolQueues = 1024;
 __device__ uint32_t g_pool_queue[2 * kPoolQueues];
 
@@ -451,27 +461,40 @@ __device__ __forceinline__ void copy_nodes_lds(const SceneView<R>& sc, rt_u4* bo
     }
 }
 
-template <class R, bool COUNT>
-__global__ __launch_bounds__(64 * lds_waves<R>(), (waves_per_simd<R, ACC_BVH_SPHERES_LDS>()))
+// ACC_GRID_LDS: the same workgroups and queue with the uniform grid's cell offsets and records
+// (binary64: the 16-B binary32 filters; binary32: the whole 32-B records) in LDS instead of nodes: the
+// filter rejections, most of a grid walk's record tests, no longer touch the vector memory path.
+template <class R, bool COUNT, int ACC>
+__global__ __launch_bounds__((64 * lds_waves<R, ACC>()), (waves_per_simd<R, ACC>()))
 void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, const int tiles, const int chunk,
                            const int items, const int qi) {
-    constexpr int ACC = ACC_BVH_SPHERES_LDS, W = lds_waves<R>();
+    constexpr int W = lds_waves<R, ACC>();
     const SceneView<R>& sc = args.sc;
-    // dynamic LDS: [child boxes 48 B x n][child references 8 B x n][W stacks of entries x 64 ints]
+    // dynamic LDS: [child boxes 48 B x n][child references 8 B x n][W stacks of entries x 64 ints], or
+    // for the grid [records][cell offsets]
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_dyn[];
     __shared__ double acc_all[W * 3 * 64];
-    const int n = sc.num_sphere_wide, entries = min(sc.stack_entries, RT_BVH_STACK);
-    rt_u4* box = reinterpret_cast<rt_u4*>(lds_dyn);
-    rt_u2* kid = reinterpret_cast<rt_u2*>(lds_dyn + 48 * n);
-    int* stacks = reinterpret_cast<int*>(lds_dyn + 56 * n);
-    copy_nodes_lds(sc, box, kid, threadIdx.x, 64 * W);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    BvhStack stk{nullptr, 0};
+    if constexpr (ACC == ACC_GRID_LDS) {
+        rt_u4* grec = reinterpret_cast<rt_u4*>(lds_dyn);
+        int* gcell = reinterpret_cast<int*>(lds_dyn + grid_lds_rec_bytes(sc));
+        copy_grid_lds(sc, grec, gcell, threadIdx.x, 64 * W);
+        stk.gcell = gcell;
+        stk.grec = grec;
+    } else {
+        const int n = sc.num_sphere_wide, entries = min(sc.stack_entries, RT_BVH_STACK);
+        rt_u4* box = reinterpret_cast<rt_u4*>(lds_dyn);
+        rt_u2* kid = reinterpret_cast<rt_u2*>(lds_dyn + 48 * n);
+        int* stacks = reinterpret_cast<int*>(lds_dyn + 56 * n);
+        copy_nodes_lds(sc, box, kid, threadIdx.x, 64 * W);
+        stk = BvhStack{stacks + wave * entries * 64 + lane, 64, box, kid};
+    }
     double* acc = acc_all + wave * 3 * 64;
     acc[lane] = 0;
     acc[64 + lane] = 0;
     acc[128 + lane] = 0;
     __syncthreads();
-    const BvhStack stk{stacks + wave * entries * 64 + lane, 64, box, kid};
     uint32_t* queue = g_pool_queue + 2 * qi;
     PixelResult res{0, 0, {0, 0, 0}, {0, 0, 0}};
     for (;;) {
@@ -575,6 +598,25 @@ size_t pool_partial_bytes(int cw, int ch, int ns, bool tri_bvh, int chunk_overri
 #ifndef RT_LDS_NODES
 #define RT_LDS_NODES 1
 #endif
+// Which grid launches read the grid from LDS (trace_pool_lds_kernel<.., ACC_GRID_LDS>): RT_LDS_GRID=0
+// never (A/B), 1 (default) whenever the copy fits
+#ifndef RT_LDS_GRID
+#define RT_LDS_GRID 1
+#endif
+template <class R>
+static size_t lds_grid_bytes(const SceneView<R>& sc) {
+    static int v = -1;
+    if (v == -1) {
+        const char* e = getenv("RT_LDS_GRID");
+        v = e ? atoi(e) : RT_LDS_GRID;
+    }
+    if (v < 1 || sc.num_grid_cells <= 0) return 0;
+    constexpr int W = lds_waves<R, ACC_GRID_LDS>();
+    const size_t b = (grid_lds_bytes(sc) + 15) & ~(size_t)15;
+    const size_t budget = 160 * 1024 / (4 * waves_per_simd<R, ACC_GRID_LDS>() / W);
+    return b + (size_t)W * 3 * 64 * 8 + 256 <= budget ? b : 0;
+}
+
 // LDS of trace_pool_lds_kernel (dynamic part), 0 if not used for this scene or if its sphere tree does
 // not fit: the kernel's workgroups per CU share its 160 KiB
 template <class R>
@@ -606,16 +648,17 @@ static int device_cus() {
 template <class R, int ACC>
 static void launch_pool_kernel(const TraceArgs<R>& a, bool count, double* part, int tiles, int chunks, int chunk,
                                hipStream_t stream) {
-    if constexpr (ACC == ACC_BVH_SPHERES) {
-        const size_t lb = lds_nodes_bytes(a.sc);
+    if constexpr (ACC == ACC_BVH_SPHERES || ACC == ACC_GRID) {
+        constexpr int LACC = ACC == ACC_GRID ? ACC_GRID_LDS : ACC_BVH_SPHERES_LDS;
+        const size_t lb = ACC == ACC_GRID ? lds_grid_bytes(a.sc) : lds_nodes_bytes(a.sc);
         if (lb) {
             const int qi = (int)(g_next_queue++ % kPoolQueues);
             const long long items = (long long)tiles * chunks;
-            constexpr int W = lds_waves<R>();
-            const int resident = device_cus() * 4 * waves_per_simd<R, ACC_BVH_SPHERES_LDS>() / W;
+            constexpr int W = lds_waves<R, LACC>();
+            const int resident = device_cus() * 4 * waves_per_simd<R, LACC>() / W;
             const int grid = (int)std::min<long long>(resident, (items + W - 1) / W);
-            if (count) hipLaunchKernelGGL((trace_pool_lds_kernel<R, true>), dim3(grid), dim3(64 * W), lb, stream, a, part, tiles, chunk, (int)items, qi);
-            else hipLaunchKernelGGL((trace_pool_lds_kernel<R, false>), dim3(grid), dim3(64 * W), lb, stream, a, part, tiles, chunk, (int)items, qi);
+            if (count) hipLaunchKernelGGL((trace_pool_lds_kernel<R, true, LACC>), dim3(grid), dim3(64 * W), lb, stream, a, part, tiles, chunk, (int)items, qi);
+            else hipLaunchKernelGGL((trace_pool_lds_kernel<R, false, LACC>), dim3(grid), dim3(64 * W), lb, stream, a, part, tiles, chunk, (int)items, qi);
             return;
         }
     }
@@ -796,6 +839,30 @@ __global__ __launch_bounds__(64) void closest_hits_lds_kernel(const SceneView<R>
     idx_out[r] = c.kind == HIT_NONE ? -1 : c.idx;
 }
 
+// ... through the LDS copy of the grid (the walk of trace_pool_lds_kernel<.., ACC_GRID_LDS>)
+template <class R>
+__global__ __launch_bounds__(64) void closest_hits_grid_lds_kernel(const SceneView<R> sc, const double* __restrict__ rays,
+                                                                   const size_t n, double* __restrict__ t_out,
+                                                                   int* __restrict__ kind_out, int* __restrict__ idx_out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_dyn[];   // [records][cell offsets]
+    BvhStack stk{nullptr, 0};
+    rt_u4* grec = reinterpret_cast<rt_u4*>(lds_dyn);
+    int* gcell = reinterpret_cast<int*>(lds_dyn + grid_lds_rec_bytes(sc));
+    copy_grid_lds(sc, grec, gcell, threadIdx.x, 64);
+    __syncthreads();
+    stk.gcell = gcell;
+    stk.grec = grec;
+    const size_t r = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (r >= n) return;
+    const double* q = rays + 6 * r;
+    const V3<R> o = mk<R>((R)q[0], (R)q[1], (R)q[2]), d = mk<R>((R)q[3], (R)q[4], (R)q[5]);
+    Work w{0, 0, 0, 0, 0, 0};
+    const Closest<R> c = closest_hit_acc<R, ACC_GRID_LDS>(sc, o, d, w, stk);
+    t_out[r] = c.kind == HIT_NONE ? (double)INFINITY : (double)c.t;
+    kind_out[r] = c.kind;
+    idx_out[r] = c.kind == HIT_NONE ? -1 : c.idx;
+}
+
 template <class R>
 hipError_t launch_closest_hits(const SceneView<R>& sc, bool bvh, const double* rays, size_t n, double* t, int* kind,
                                int* idx, hipStream_t stream) {
@@ -807,6 +874,8 @@ hipError_t launch_closest_hits(const SceneView<R>& sc, bool bvh, const double* r
         hipLaunchKernelGGL((closest_hits_lds_kernel<R>), grid, dim3(64), lb, stream, sc, rays, n, t, kind, idx);
     } else if (spheres)
         hipLaunchKernelGGL((closest_hits_kernel<R, ACC_BVH_SPHERES>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);
+    else if (bvh && bvh_walk_mode(sc) == ACC_GRID && lds_grid_bytes(sc))
+        hipLaunchKernelGGL((closest_hits_grid_lds_kernel<R>), grid, dim3(64), lds_grid_bytes(sc), stream, sc, rays, n, t, kind, idx);
     else if (bvh && bvh_walk_mode(sc) == ACC_GRID)
         hipLaunchKernelGGL((closest_hits_kernel<R, ACC_GRID>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);
     else if (bvh) hipLaunchKernelGGL((closest_hits_kernel<R, ACC_BVH_STACK>), grid, dim3(64), 0, stream, sc, rays, n, t, kind, idx);

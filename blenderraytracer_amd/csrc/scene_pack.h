@@ -605,6 +605,7 @@ void fill_view_constants(SceneView<R>& v, const HostScene& hs, const rt_scene_de
     v.num_tri_wide = (int)hs.tri_wide.size();
     v.num_big_spheres = (int)hs.big_spheres.size();
     v.num_grid_cells = hs.grid_n[0] * hs.grid_n[1] * hs.grid_n[2];
+    v.num_grid_recs = (int)hs.grid_ids.size();
     for (int k = 0; k < 3; ++k) {
         v.grid_n[k] = hs.grid_n[k];
         v.grid_lo[k] = hs.grid_lo[k];
@@ -678,7 +679,7 @@ inline void choose_walk(HostScene& hs, const rt_scene_desc& d) {
             for (int bounce = 0; bounce < 2; ++bounce) {
                 Work wt{}, wg{};
                 const Closest<double> h = closest_hit_bvh<double, true, false>(v, o, dir, wt, BvhStack{stack, 1});
-                closest_hit_grid<double>(v, o, dir, wg);
+                closest_hit_grid<double>(v, o, dir, wg, BvhStack{stack, 1});
                 tree += wt.nodes + 0.5 * wt.spheres;
                 grid += wg.nodes + 0.5 * wg.spheres;
                 if (h.kind == HIT_NONE) break;

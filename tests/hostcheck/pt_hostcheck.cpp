@@ -249,6 +249,9 @@ extern "C" long long ptc_bvh_check(const rt_scene_desc* d, long long n, unsigned
     const SceneView<double>& v = hv.v;
     std::vector<double> rays(6 * (size_t)std::max(0LL, n));
     const long long m = bvh_rays(hv.hs, n, seed, rays.data());
+    std::vector<rt_u4> grid_rec_copy(grid_lds_rec_bytes(v) / 16 + 1);
+    std::vector<int> grid_cell_copy((size_t)v.num_grid_cells + 1);
+    if (v.num_grid_cells > 0) copy_grid_lds(v, grid_rec_copy.data(), grid_cell_copy.data(), 0, 1);
     long long bad = 0, nh = 0;
     for (long long it = 0; it < m; ++it) {
         const double* r = &rays[6 * it];
@@ -258,10 +261,15 @@ extern "C" long long ptc_bvh_check(const rt_scene_desc* d, long long n, unsigned
         int stack[RT_BVH_STACK];
         const Closest<double> b = closest_hit_bvh<double, false>(v, O, D, w, BvhStack{nullptr, 0});
         const Closest<double> c = closest_hit_bvh<double, true>(v, O, D, w, BvhStack{stack, 1});
-        const Closest<double> g = v.num_grid_cells > 0 && v.num_tri_nodes == 0
-                                      ? closest_hit_grid<double>(v, O, D, w) : c;
+        const bool grid = v.num_grid_cells > 0 && v.num_tri_nodes == 0;
+        const Closest<double> g = grid ? closest_hit_grid<double>(v, O, D, w, BvhStack{stack, 1}) : c;
+        // the LDS-copy form of the grid walk (ACC_GRID_LDS) over a host copy of the grid
+        BvhStack gs{stack, 1};
+        gs.gcell = grid_cell_copy.data();
+        gs.grec = grid_rec_copy.data();
+        const Closest<double> gl = grid ? closest_hit_grid<double, true>(v, O, D, w, gs) : c;
         if (a.kind != HIT_NONE) ++nh;
-        for (const Closest<double>& x : {b, c, g}) {
+        for (const Closest<double>& x : {b, c, g, gl}) {
             const bool same = a.kind == x.kind && (a.kind == HIT_NONE || (a.idx == x.idx && a.mat == x.mat &&
                                                                          std::memcmp(&a.t, &x.t, 8) == 0));
             bad += !same;
