@@ -611,6 +611,7 @@ void fill_view_constants(SceneView<R>& v, const HostScene& hs, const rt_scene_de
         v.grid_lo[k] = hs.grid_lo[k];
         v.grid_hi[k] = hs.grid_hi[k];
         v.grid_cs[k] = hs.grid_cs[k];
+        v.grid_ics[k] = hs.grid_cs[k] > 0.0f ? 1.0f / hs.grid_cs[k] : 0.0f;
     }
     v.grid_far = hs.grid_far;
     v.use_grid = hs.use_grid ? 1 : 0;

@@ -363,6 +363,20 @@ def test_lds_node_kernel_bit_identical(gpu, tmp_path, env):
         assert np.array_equal(lds[k], again[k], equal_nan=True), k
 
 
+@pytest.mark.parametrize("env", [{}, {"RT_PART_MB": "1", "RT_POOL_CHUNK": "2"}], ids=["default", "split_launches"])
+def test_lds_grid_kernel_bit_identical(gpu, tmp_path, env):
+    """The grid walk with its cell offsets and record filters in LDS (trace_pool_lds_kernel<.., 7>,
+    default where the grid is walked: RTOW in both precisions) renders exactly the bits of the one-wave
+    grid kernel reading them from global memory (RT_LDS_GRID=0): sums, segment and draw counts, batched
+    renders, also over many launches, and again in a second process."""
+    base = _render_in_child(_POOL_SCRIPT, tmp_path / "global.npz", RT_LDS_GRID="0", **env)
+    lds = _render_in_child(_POOL_SCRIPT, tmp_path / "lds.npz", RT_LDS_GRID="1", **env)
+    again = _render_in_child(_POOL_SCRIPT, tmp_path / "again.npz", **env)
+    for k in base.files:
+        assert np.array_equal(base[k], lds[k], equal_nan=True), k
+        assert np.array_equal(lds[k], again[k], equal_nan=True), k
+
+
 @pytest.mark.parametrize("precision", [capi.RT_PREC_F64, capi.RT_PREC_F32], ids=["f64", "f32"])
 def test_trace_device_two_streams_then_render(gpu, precision):
     """Scene scratch shared across streams: two rt_trace_device shards enqueued on two
@@ -567,12 +581,16 @@ np.savez(sys.argv[2], bt=bt, bk=bk, bi=bi, vt=vt, vk=vk, vi=vi)
 '''
 
 
-@pytest.mark.parametrize("walk", ["tree", "grid"])
+@pytest.mark.parametrize("walk", ["tree", "grid", "grid_global"])
 def test_rtow_walks_closest_hit_identical_on_device(gpu, tmp_path, walk):
-    """RTOW's two sphere walks, each forced in a child process (the trace kernel uses the grid there),
-    on the host check's 200k adversarial rays through rt_closest_hits: device walk == device World
-    order, bit for bit (t, kind, index)."""
-    res = _render_in_child(_TREE_PROOF_SCRIPT, tmp_path / f"{walk}.npz", RT_BVH_WALK=walk)
+    """RTOW's two sphere walks, each forced in a child process (the trace kernel uses the grid there,
+    its records in LDS; grid_global: read from global memory, RT_LDS_GRID=0), on the host check's 200k
+    adversarial rays through rt_closest_hits: device walk == device World order, bit for bit (t, kind,
+    index)."""
+    env = {"RT_BVH_WALK": walk.split("_")[0]}
+    if walk == "grid_global":
+        env["RT_LDS_GRID"] = "0"
+    res = _render_in_child(_TREE_PROOF_SCRIPT, tmp_path / f"{walk}.npz", **env)
     assert (res["bk"] >= 0).sum() > len(res["bk"]) // 10
     assert np.array_equal(res["bk"], res["vk"]) and np.array_equal(res["bi"], res["vi"])
     assert np.array_equal(res["bt"].view(np.uint64), res["vt"].view(np.uint64))
