@@ -12,7 +12,7 @@ from blenderraytracer_amd import capi
 from oracle import binding
 
 
-@pytest.mark.parametrize("case", gc.case_names())
+@pytest.mark.parametrize("case", gc.case_names(heavy=False))   # heavy cases: the BVH walks below
 def test_kernel_logic_f64_matches_reference(case):
     rt, c = gc.tracer_for(case)
     r = hb.render(rt.packed(), rt.settings(crop=c["crop"]))

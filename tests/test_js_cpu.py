@@ -24,11 +24,11 @@ pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
 def js_outputs(tmp_path_factory):
     gc.ensure_mesh50k_file()                       # generated on demand (git-ignored)
     out = tmp_path_factory.mktemp("jscpu")
-    subprocess.run([NODE, TOOL, "golden", str(out), *gc.case_names()], check=True, timeout=900)
+    subprocess.run([NODE, TOOL, "golden", str(out), *gc.case_names(heavy=False)], check=True, timeout=900)
     return out
 
 
-@pytest.mark.parametrize("case", gc.case_names())
+@pytest.mark.parametrize("case", gc.case_names(heavy=False))
 def test_js_cpu_path_bit_exact(js_outputs, case):
     c = gc.manifest()["cases"][case]
     _, _, cw, ch = c["crop"]
