@@ -14,8 +14,10 @@ N > 1, two ways, both runnable as a plain `python bench.py --gpus 
       torch.distributed.run (WORLD_SIZE set) this process is one rank; without it, this process starts
       the N rank processes itself (before touching any GPU) and exits with rank 0's status.
   --mp-mode inproc: one process, rt_settings.devices = [0..N-1] — the split the Node drop-in ships
-      (installGpuRender(rt, {devices})): replicas of the scene, peer copies of the sums over xGMI to
-      device 0, the epilogue there; a step is one rt_render call delivering RGBA8 to the host.
+      (installGpuRender(rt, {devices})): replicas of the scene, whole sample batches round-robin over
+      the devices, each batch's chunk partials copied over xGMI to device 0 and reduced there in batch
+      order, the epilogue there; a step is one rt_render call delivering RGBA8 to the host.  The line
+      also carries `progressive_16`: the same with the Node default of 16 progressive batches.
 
 Prints ONE JSON line on rank 0 (driver contract).  The trace step's duration comes from HIP events
 recorded inside librt_hip.so on the stream the kernels run on.  At N=1 (unless --no-pmc) rank 0 then
@@ -205,16 +207,18 @@ def pmc_passes(args, outdir):
         files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
         if not files:
             return {"error": f"{name} pass wrote no counter_collection.csv"}
-        tot, per_kernel = {}, {}
+        tot, per_kernel, names = {}, {}, []
         for row in csv.DictReader(open(files[0])):
             k = next((k for k in TRACE_KERNELS if k in row["Kernel_Name"]), None)
             if k is None:
                 continue
+            if row["Kernel_Name"] not in names:
+                names.append(row["Kernel_Name"])
             v = float(row["Counter_Value"])
             tot[row["Counter_Name"]] = tot.get(row["Counter_Name"], 0.0) + v
             per_kernel.setdefault(k, {})
             per_kernel[k][row["Counter_Name"]] = per_kernel[k].get(row["Counter_Name"], 0.0) + v
-        res[name] = {"total": tot, "per_kernel": per_kernel, "csv": os.path.relpath(files[0], ROOT)}
+        res[name] = {"total": tot, "per_kernel": per_kernel, "names": names, "csv": os.path.relpath(files[0], ROOT)}
     return res
 
 
@@ -303,6 +307,9 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and args.mp_mode == "ranks":
         raise SystemExit(spawn_ranks(args))
     inproc = args.gpus > 1 and args.mp_mode == "inproc"
+    # under torch.distributed.run (WORLD_SIZE set) the process group is up at every world size, 1
+    # included: the sums then go through the RCCL reduce even on one GPU (tests/test_gpu_parity.py)
+    distributed = not inproc and "WORLD_SIZE" in os.environ
     world = 1 if inproc else int(os.environ.get("WORLD_SIZE", "1"))
     rank = 0 if inproc else int(os.environ.get("RANK", "0"))
     local = 0 if inproc else int(os.environ.get("LOCAL_RANK", "0"))
@@ -312,7 +319,7 @@ def main():
     if args.dist_backend == "gloo":
         local %= ndev
     torch.cuda.set_device(local)
-    if world > 1:
+    if distributed:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -335,24 +342,53 @@ def main():
     for _ in range(args.warmup):
         job.step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
-    kernel_ms, segs, abytes, work = [], [], [], []
+    # ranks: no host synchronization inside a timed step — the trace's duration comes from HIP events
+    # recorded around it on the stream it runs on (torch's current stream, handed to rt_trace_device);
+    # inproc: rt_render is synchronous and reports its own HIP-event time
+    kernel_ms = []
+    events = [] if inproc else [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                                for _ in range(args.steps)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        job.step()
-        kernel_ms.append(job.stats.kernel_ms)
-        segs.append(job.stats.segments)
-        abytes.append(job.stats.algorithmic_bytes)
-        work.append((job.stats.node_visits, job.stats.sphere_tests, job.stats.tri_tests))
+    for k in range(args.steps):
+        if inproc:
+            job.step()
+            kernel_ms.append(job.stats.kernel_ms)
+        else:
+            job.step(stats=False, events=events[k])
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if not inproc:
+        kernel_ms = [a.elapsed_time(b) for a, b in events]
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
-    if world > 1:
+    if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    # the work counters of the frame (identical in every step): one more, untimed step with stats
+    job.step()
+    torch.cuda.synchronize()
+    segs, abytes = [job.stats.segments], [job.stats.algorithmic_bytes]
+    work = [(job.stats.node_visits, job.stats.sphere_tests, job.stats.tri_tests)]
+    progressive = None
+    if inproc:
+        # the Node drop-in's default: 16 progressive batches with a running frame and a progress call
+        # after each (gpu-ray-tracer.mjs DEFAULT_PROGRESS_STEPS), timed over the same number of steps
+        from blenderraytracer_amd.distributed import InProcessRender
+        pj = InProcessRender(rt, inproc_devices, progress_steps=16)
+        pj.step()
+        tp = time.perf_counter()
+        for _ in range(args.steps):
+            pj.step()
+        pt = time.perf_counter() - tp
+        progressive = {"value": round(cfg["w"] * cfg["h"] * rt.settings().samples * args.steps / pt / 1e6, 3),
+                       "unit": "Msamples/s", "ms_per_step": round(pt / args.steps * 1e3, 3), "batches": 16,
+                       "batch_samples": pj.batch, "progress_calls_per_step": pj.progress_calls // (args.steps + 1),
+                       "what": "rt_render with rt_settings.devices as the Node drop-in ships it: 16 sample batches "
+                               "dealt round-robin to the devices, the running frame into a preview buffer and a "
+                               "progress callback after each batch"}
     if args.dump and rank == 0:
         import numpy as np
         torch.cuda.synchronize()
@@ -394,8 +430,10 @@ def main():
             capi.load_library().rt_scene_walk(rt.scene_handle(), capi.RT_PREC_F32 if args.precision == "f32" else capi.RT_PREC_F64,
                                               {"auto": capi.RT_ACCEL_AUTO, "brute": capi.RT_ACCEL_BRUTE, "bvh": capi.RT_ACCEL_BVH}[args.accel]),
             "error")
-        kernel_desc = ("trace step: trace_pool_kernel (trace_pool_lds_kernel for binary32 sphere scenes) + "
-                       "reduce_kernel (one launch each per frame)")
+        kernel_desc = ("trace step of the " + walk + " walk: " +
+                       ("trace_pool_lds_kernel (the grid's cell offsets and filters in LDS, when they fit)"
+                        if walk == "uniform_grid" else "trace_pool_kernel / trace_pool_lds_kernel") +
+                       " + reduce_kernel, one launch each per frame; the counter pass names the kernels it saw")
         roofline = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                     "traffic": None, "kernel": kernel_desc, "kernel_ms": round(k_ms, 3)}
         binding = vmem = None
@@ -410,6 +448,7 @@ def main():
             if "error" in pmc:
                 roofline["pmc_error"] = pmc["error"]
             else:
+                roofline["kernel"] = " + ".join(pmc["fetch"]["names"]) + " (the kernels the counter passes saw)"
                 fetch = 2.0 * pmc["fetch"]["total"].get("FETCH_SIZE", 0.0) * 1024   # gfx950: x2, KiB
                 write = pmc["write"]["total"].get("WRITE_SIZE", 0.0) * 1024
                 hbm = fetch + write
@@ -456,6 +495,9 @@ def main():
         roofline.update({
             "cache_served_bytes": a_bytes,
             "cache_served_GBps": round(a_bytes / (k_ms * 1e-3) / 1e9, 2),
+            "algorithmic_frac": round(a_bytes / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "algorithmic_frac_definition": "cache_served_GBps / 8000: the SURVEY 8d bytes of the work done, served "
+                                           "from LDS/L1/L2, NOT HBM traffic (that is `frac`)",
             "cache_served_definition": ("SURVEY 8d algorithmic bytes, BVH form: 64 B/node visited (8 B/cell for the "
                                         "uniform-grid walk) + 16 B/sphere + 36 B/triangle tested + segments x 24 "
                                         "B/plane|box + 12 B/pixel; read from L1/L2 (the trees are cache-resident), "
@@ -465,15 +507,16 @@ def main():
             "walk": walk,
             "walk_steps_per_segment": round(nodes / seg_launch, 3) if bvh else None,
             "prim_tests_per_segment": round((sph + tri) / seg_launch, 3) if bvh else None})
-        if world > 1:
+        if distributed:
             mp_mode = {"mode": "ranks", "world_size": dist.get_world_size(), "backend": dist.get_backend(),
                        "launcher": "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else "bench.py spawn"}
-            parallelism = (f"sample-split x{world} + RCCL reduce" if args.dist_backend == "nccl" else
+            parallelism = (f"sample-split x{world} + RCCL reduce" if args.dist_backend == "nccl" and world > 1 else
+                           "1 GPU, RCCL reduce at world size 1" if args.dist_backend == "nccl" else
                            f"REHEARSAL sample-split x{world} over {ndev} GPU(s), gloo host reduce: not a measurement")
         elif inproc:
             mp_mode = {"mode": "inproc", "devices": inproc_devices}
-            parallelism = (f"in-process sample-split x{args.gpus} (rt_settings.devices {inproc_devices}: peer copies "
-                           "over xGMI + add on device 0)" +
+            parallelism = (f"in-process whole-batch split x{args.gpus} (rt_settings.devices {inproc_devices}: batch k "
+                           "on device k % N, chunk partials copied over xGMI and reduced in batch order on device 0)" +
                            ("" if len(set(inproc_devices)) == args.gpus else
                             f": REHEARSAL on {ndev} GPU(s), not a measurement"))
         else:
@@ -489,6 +532,7 @@ def main():
                        "max_depth": cfg["depth"], "primitives": packed.primitives_per_segment(), "accel": args.accel,
                        "parallelism": parallelism},
             "mp_mode": mp_mode,
+            "progressive_16": progressive,
             "roofline": roofline,
             "roofline_binding": binding,
             "roofline_vmem": vmem,
@@ -504,7 +548,7 @@ def main():
             "build": build_provenance(),
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

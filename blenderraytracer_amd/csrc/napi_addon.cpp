@@ -5,7 +5,7 @@
 //   createScene(desc, device)          -> External   (rt_scene_create: scene copied into HBM)
 //   render(scene, settings, progress?) -> Promise<{mean?, post?, rgba8, segments?, draws?, stats}>
 //                                         (rt_render on a libuv worker thread: the event loop stays live)
-//   cancel(scene)                      -> rt_cancel (polled between sample batches)
+//   cancel(scene)                      -> rt_cancel (the queued batches stop at their next item)
 //   destroyScene(scene), deviceCount(), abiVersion()
 // Progress reaches JS through a napi_threadsafe_function, in order and before the Promise settles (the
 // worker waits until the main thread has run each call, as the reference calls onProgress inside its

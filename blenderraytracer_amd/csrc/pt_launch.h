@@ -22,6 +22,25 @@ struct Counters {
     unsigned long long* totals;   // optional [segments, BVH nodes, sphere tests, triangle tests]
     double* part = nullptr;    // sample-pool chunk partials (scratch, pool_partial_bytes)
     size_t part_bytes = 0;
+    // progressive renders (render_impl): the render's cancel word in mapped host memory, read by the pool
+    // kernels before every (tile, chunk) item; a wave that finds it set leaves its items untraced and
+    // sets *aborted (this batch's word, mapped host memory too), so that the batch is never reduced
+    const uint32_t* cancel = nullptr;
+    uint32_t* aborted = nullptr;
+};
+
+// The commit of one batch's chunk partials (render_impl with a cancel word): a one-thread gate kernel
+// before the reduce reads the batch's `aborted` word and the render's sticky `stop` word (both mapped
+// host memory); if either is set the batch is not added (and `stop` is set, so no later batch is
+// either: the sums always hold a prefix of the batches), else `done` = done_value (the samples the sums
+// hold once this reduce has run).  The decision goes to `skip` (device memory), which every reduce
+// thread reads, so that the host-memory words are read once per batch.
+struct ReduceGate {
+    const uint32_t* aborted = nullptr;
+    uint32_t* stop = nullptr;
+    int32_t* done = nullptr;
+    int32_t done_value = 0;
+    uint32_t* skip = nullptr;
 };
 
 // bvh: walk the BVHs (ACC_BVH_STACK, the ordered two-child walk), else World order (ACC_BRUTE).
@@ -40,7 +59,8 @@ PoolPlan pool_plan(int cw, int ch, int ns, bool tri_bvh, int chunk = 0);
 template <class R>
 hipError_t launch_trace_partials(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh,
                                  double* part, size_t part_bytes, hipStream_t stream);
-hipError_t launch_reduce(const ImageParams& im, double* sum, const double* part, bool tri_bvh, hipStream_t stream);
+hipError_t launch_reduce(const ImageParams& im, double* sum, const double* part, bool tri_bvh, hipStream_t stream,
+                         const ReduceGate* gate = nullptr);
 
 // World.hit of n rays (n x 6 doubles, device) -> t, kind, index (device): rt_closest_hits
 template <class R>

@@ -107,6 +107,16 @@ __device__ __forceinline__ void add_totals(const Counters& c, const PixelResult&
     }
 }
 
+// The render's cancel word (Counters::cancel, mapped host memory written by rt_cancel / the progress
+// callback): read with system scope, so the read goes to host memory and not to a cached copy.
+__device__ __forceinline__ bool cancel_requested(const Counters& c) {
+    return c.cancel && __hip_atomic_load(const_cast<uint32_t*>(c.cancel), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
+// this batch leaves items untraced: its partials must not be reduced (one lane writes)
+__device__ __forceinline__ void mark_aborted(const Counters& c) {
+    __hip_atomic_store(c.aborted, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // 8x8 tile `tile` of the crop: origin, valid width and valid pixel count (edge tiles are ragged)
 struct Tile { int x0, y0, vw, nv; };
 __device__ __forceinline__ Tile tile_of(const ImageParams& im, int tile) {
@@ -220,6 +230,10 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
     acc[64 + lane] = 0;
     acc[128 + lane] = 0;
     __syncthreads();
+    if (args.c.cancel && __builtin_amdgcn_readfirstlane((int)cancel_requested(args.c))) {
+        if (lane == 0) mark_aborted(args.c);  // the workgroup is one item: it is left untraced
+        return;
+    }
     const int ci = blockIdx.x / tiles, tile = blockIdx.x % tiles;
     const Tile tl = tile_of(im, tile);
     const int vw = tl.vw, nv = tl.nv;
@@ -499,9 +513,17 @@ void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, c
     PixelResult res{0, 0, {0, 0, 0}, {0, 0, 0}};
     for (;;) {
         uint32_t it = 0;
-        if (lane == 0) it = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int stop = 0;
+        if (lane == 0) {
+            stop = cancel_requested(args.c);
+            it = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         it = (uint32_t)__builtin_amdgcn_readfirstlane((int)it);
         if (it >= (uint32_t)items) break;
+        if (__builtin_amdgcn_readfirstlane(stop)) {   // a cancel: this item (and the rest) stay untraced
+            if (lane == 0) mark_aborted(args.c);
+            break;
+        }
         pool_item<R, COUNT, ACC>(args, part, tiles, chunk, it, acc, stk, res, lane);
     }
     add_totals<ACC>(args.c, res, lane);
@@ -520,9 +542,9 @@ void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, c
 // workgroup waits for four free wave slots on one CU and was measured to take 7.8 ms instead of 0.1.
 __global__ __launch_bounds__(64) void reduce_kernel(const ImageParams im, double* __restrict__ sum,
                                                     const double* __restrict__ part, const int tiles,
-                                                    const int chunks) {
+                                                    const int chunks, const uint32_t* __restrict__ skip) {
     const int tile = blockIdx.x, m = threadIdx.x;
-    if (tile >= tiles) return;
+    if (tile >= tiles || (skip && *skip)) return;
     const Tile t = tile_of(im, tile);
     if (m >= t.nv) return;
     const size_t q = (size_t)(t.y0 + m / t.vw) * im.cw + (t.x0 + m % t.vw);
@@ -535,6 +557,17 @@ __global__ __launch_bounds__(64) void reduce_kernel(const ImageParams im, double
         a2 += p[128];
     }
     sum[3 * q] = a0; sum[3 * q + 1] = a1; sum[3 * q + 2] = a2;
+}
+
+// ReduceGate (pt_launch.h): whether the batch's reduce runs; one lane does the host-memory traffic
+__global__ __launch_bounds__(64) void reduce_gate_kernel(const ReduceGate g) {
+    if (threadIdx.x != 0) return;
+    const uint32_t a = __hip_atomic_load(const_cast<uint32_t*>(g.aborted), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t s = __hip_atomic_load(g.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t skip = (a | s) ? 1u : 0u;
+    *g.skip = skip;
+    if (skip) __hip_atomic_store(g.stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else __hip_atomic_store(g.done, g.done_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 bool trace_uses_pool() {
@@ -694,7 +727,7 @@ static hipError_t launch_pool(const TraceArgs<R>& a0, bool count, hipStream_t st
         launch_pool_kernel<R, ACC>(a, count, part, tiles, chunks, chunk, stream);
         if (part)
             hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)tiles), dim3(64), 0, stream, a.im, a.c.sum,
-                               (const double*)part, tiles, chunks);
+                               (const double*)part, tiles, chunks, (const uint32_t*)nullptr);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -791,10 +824,13 @@ template hipError_t launch_trace_partials<double>(const SceneView<double>&, cons
 template hipError_t launch_trace_partials<float>(const SceneView<float>&, const ImageParams&, const Counters&, bool,
                                                  double*, size_t, hipStream_t);
 
-hipError_t launch_reduce(const ImageParams& im, double* sum, const double* part, bool tri_bvh, hipStream_t stream) {
+hipError_t launch_reduce(const ImageParams& im, double* sum, const double* part, bool tri_bvh, hipStream_t stream,
+                         const ReduceGate* gate) {
     if (im.cw <= 0 || im.ch <= 0 || im.s_end <= im.s_begin) return hipSuccess;
     const PoolPlan p = pool_plan(im.cw, im.ch, im.s_end - im.s_begin, tri_bvh, im.pool_chunk);
-    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)p.tiles), dim3(64), 0, stream, im, sum, part, p.tiles, p.chunks);
+    if (gate) hipLaunchKernelGGL(reduce_gate_kernel, dim3(1), dim3(64), 0, stream, *gate);
+    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)p.tiles), dim3(64), 0, stream, im, sum, part, p.tiles, p.chunks,
+                       (const uint32_t*)(gate ? gate->skip : nullptr));
     return hipGetLastError();
 }
 

@@ -145,11 +145,21 @@ double now_ms() {
     return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
 }
 
-// Batches in flight per render (render_impl): kSlots partial slots / trace streams; the host queues up
-// to kSlots batches beyond the one it waits for, each with its own preview staging and completion event
-// (kDone of them, so a queued batch never writes a frame the host has not read yet).
+// Batches in flight per render (render_impl): kSlots partial slots / trace streams per device; the host
+// queues up to kSlots batches per device beyond the one it waits for (lookahead()), each with its own
+// preview staging and completion event (lookahead() + kSlots of them, so a queued batch never writes a
+// frame the host has not read yet).
 constexpr int kSlots = 3;
-constexpr int kDone = 2 * kSlots;
+inline int lookahead(int devices) { return kSlots * std::max(1, devices); }
+
+// The render's control words (rt_scene::ctl, mapped coherent host memory, read and written by the host
+// and by the kernels of every device): the cancel word, the sticky stop word and the samples the sums
+// hold (ReduceGate), and one `aborted` word per batch slot of the ring.
+constexpr int kCtlCancel = 0, kCtlStop = 1, kCtlDone = 2, kCtlAborted = 4;
+constexpr int kCtlWords = kCtlAborted + 64;
+static_assert(kCtlAborted + kSlots * RT_MAX_DEVICES + kSlots <= kCtlWords, "one aborted word per ring slot");
+inline uint32_t ctl_load(const uint32_t* ctl, int k) { return __atomic_load_n(ctl + k, __ATOMIC_SEQ_CST); }
+inline void ctl_store(uint32_t* ctl, int k, uint32_t v) { __atomic_store_n(ctl + k, v, __ATOMIC_SEQ_CST); }
 
 // Everything one device holds for a scene: the scene arrays in its HBM, a stream, the running sums
 // and counters of the samples it traces, the pool's chunk partials and the work totals (scratch).
@@ -163,6 +173,7 @@ struct DeviceState {
     DevBuf<uint32_t> segs, draws;
     DevBuf<unsigned long long> total;
     DevBuf<double> part;               // sample-pool chunk partials (ensure_partials; overlapped batches: slot 0)
+    DevBuf<uint32_t> gate_skip;        // ReduceGate::skip of the reduces on this device's stream
     hipEvent_t scratch_ev = nullptr;   // recorded after every use of part / total (order_scratch)
     hipStream_t scratch_stream = nullptr;
     bool scratch_used = false;
@@ -207,7 +218,7 @@ struct DeviceState {
         sync_all();
         s64.release();
         s32.release();
-        sum.release(); segs.release(); draws.release(); total.release(); part.release();
+        sum.release(); segs.release(); draws.release(); total.release(); part.release(); gate_skip.release();
         for (DevBuf<double>& b : part_more) b.release();
         for (hipEvent_t e : {ev[0], ev[1], setup_ev, scratch_ev, copy_ev})
             if (e) (void)hipEventDestroy(e);
@@ -239,12 +250,26 @@ struct DescCopy {
 
 }  // namespace
 
-// A shard's staging buffers on the home device and the event that frees them (merge_shards).
+// A shard's staging buffers on the home device and the events that free them (merge_shards,
+// trace_replica).
 struct MergeSlot {
     DevBuf<double> sum;
     DevBuf<uint32_t> segs, draws;
     hipEvent_t added = nullptr;     // recorded on the home stream after this slot's adds
     bool pending = false;           // `added` has been recorded
+    // whole-batch split (trace_replica): the chunk partials of the replica's batch in its partial slot j
+    // land in stage[j] on the home device, reduced there in batch order; stage_free[j] is recorded on the
+    // home stream after that reduce
+    DevBuf<double> stage[kSlots];
+    hipEvent_t stage_free[kSlots] = {};
+    bool stage_used[kSlots] = {};
+    void release() {
+        sum.release(); segs.release(); draws.release();
+        for (DevBuf<double>& b : stage) b.release();
+        if (added) (void)hipEventDestroy(added);
+        for (hipEvent_t e : stage_free)
+            if (e) (void)hipEventDestroy(e);
+    }
 };
 
 struct rt_scene {
@@ -263,11 +288,13 @@ struct rt_scene {
     DevBuf<float> post, post_raw;   // post_raw: pre-denoise floatData
     DevBuf<uint8_t> rgba;
     // rt_output.preview_rgba8: the running frame of each batch in flight, in mapped pinned host memory
-    uint8_t* preview_host[kDone] = {};
-    uint8_t* preview_dev[kDone] = {};     // the same buffers' device addresses
+    std::vector<uint8_t*> preview_host;
+    std::vector<uint8_t*> preview_dev;    // the same buffers' device addresses
     size_t preview_host_n = 0;
-    hipEvent_t batch_done[kDone] = {};    // home stream: batch k's reduce, merges and preview done (slot k % kDone)
+    std::vector<hipEvent_t> batch_done;   // home stream: batch k's reduce, merges and preview done (slot k % ring)
     std::atomic<int> cancel{0};
+    uint32_t* ctl = nullptr;        // the render's control words (kCtl*), host address
+    uint32_t* ctl_dev = nullptr;    // ... their device address (portable mapping: valid on every device)
     size_t ckpt_pixels = 0;         // progressive state of the last rt_render / rt_render_resume:
     int ckpt_done = 0;              // `home.sum` holds samples [sample_begin, ckpt_done) of ckpt_pixels pixels
 };
@@ -356,7 +383,7 @@ hipError_t trace(const rt_scene* sc, const DeviceState& ds, const rt_settings* s
 // order once the trace is done.  Sums see the same additions in the same order as trace() of the batch
 // (bit-identical), while the trace of batch k+1 may already run beside batch k's draining waves.
 hipError_t trace_overlapped(const rt_scene* sc, DeviceState& ds, const rt_settings* s, const ImageParams& im,
-                            const Counters& c, int j, bool slot_used) {
+                            const Counters& c, int j, bool slot_used, const ReduceGate* gate) {
     if (im.max_depth <= 0 || im.s_end <= im.s_begin) return hipSuccess;
     const bool bvh = use_bvh(sc, s);
     DevBuf<double>& part = ds.slot_part(j);
@@ -369,20 +396,87 @@ hipError_t trace_overlapped(const rt_scene* sc, DeviceState& ds, const rt_settin
                 : launch_trace_partials<double>(ds.s64.view, im, c, bvh, part.p, part.n * sizeof(double), ts);
     if (e == hipSuccess) e = hipEventRecord(ds.traced[j], ts);
     if (e == hipSuccess) e = hipStreamWaitEvent(ds.stream, ds.traced[j], 0);
-    if (e == hipSuccess) e = launch_reduce(im, c.sum, part.p, sc->tri_bvh, ds.stream);
+    if (e == hipSuccess) e = launch_reduce(im, c.sum, part.p, sc->tri_bvh, ds.stream, gate);
     if (e == hipSuccess) e = hipEventRecord(ds.reduced[j], ds.stream);
     return e;
 }
 
+// One whole batch on a replica (the whole-batch split of render_impl): the pool kernel writes the
+// batch's chunk partials into the replica's slot j on its tstream[j]; the same stream then copies them
+// into the home device's staging slot j (once the home stream's last reduce of that slot is done), and
+// the home stream adds them to the home sums in chunk order after the copy — exactly the reduce that
+// trace_overlapped runs for a batch traced on the home device, in the same (batch) order, so the sums
+// are bit-identical to the same batches on one device.  The replica's next trace into slot j follows
+// the copy on the same stream.
+int trace_replica(rt_scene* sc, DeviceState& ds, MergeSlot& m, const rt_settings* s, const ImageParams& im,
+                  const Counters& c, int j, const ReduceGate* gate) {
+    if (im.max_depth <= 0 || im.s_end <= im.s_begin) return RT_OK;
+    DeviceState& h = sc->home;
+    const int cw = im.cw, ch = im.ch;
+    const size_t bytes = pool_plan(cw, ch, im.s_end - im.s_begin, sc->tri_bvh, im.pool_chunk).part_bytes;
+    const bool bvh = use_bvh(sc, s);
+    DevBuf<double>& part = ds.slot_part(j);
+    hipStream_t ts = ds.tstream[j];
+    HIP_TRY(hipSetDevice(h.device));
+    HIP_TRY(m.stage[j].ensure(bytes / sizeof(double)));
+    if (!m.stage_free[j]) HIP_TRY(hipEventCreateWithFlags(&m.stage_free[j], hipEventDisableTiming));
+    HIP_TRY(hipSetDevice(ds.device));
+    HIP_TRY(s->precision == RT_PREC_F32
+                ? launch_trace_partials<float>(ds.s32.view, im, c, bvh, part.p, part.n * sizeof(double), ts)
+                : launch_trace_partials<double>(ds.s64.view, im, c, bvh, part.p, part.n * sizeof(double), ts));
+    if (m.stage_used[j]) HIP_TRY(hipStreamWaitEvent(ts, m.stage_free[j], 0));
+    HIP_TRY(hipMemcpyPeerAsync(m.stage[j].p, h.device, part.p, ds.device, bytes, ts));
+    HIP_TRY(hipEventRecord(ds.traced[j], ts));              // trace + copy out done
+    HIP_TRY(hipSetDevice(h.device));
+    HIP_TRY(hipStreamWaitEvent(h.stream, ds.traced[j], 0));
+    HIP_TRY(launch_reduce(im, h.sum.p, m.stage[j].p, sc->tri_bvh, h.stream, gate));
+    HIP_TRY(hipEventRecord(m.stage_free[j], h.stream));
+    m.stage_used[j] = true;
+    return RT_OK;
+}
+
+// The per-pixel counters (segments, draws) of the replicas of a whole-batch split, added into the home
+// device's once all their batches are traced (integer sums: any order).  The replica's accumulation
+// stream first waits for its trace streams.
+int merge_counters(rt_scene* sc, const std::vector<DeviceState*>& states, size_t n, bool segs, bool draws) {
+    DeviceState& h = sc->home;
+    for (size_t k = 0; k < states.size(); ++k) {
+        DeviceState* ds = states[k];
+        if (ds == &h || !(segs || draws)) continue;
+        MergeSlot& m = sc->merge[k];
+        HIP_TRY(hipSetDevice(h.device));
+        if (segs) HIP_TRY(m.segs.ensure(n));
+        if (draws) HIP_TRY(m.draws.ensure(n));
+        HIP_TRY(hipSetDevice(ds->device));
+        if (segs) HIP_TRY(hipMemcpyPeerAsync(m.segs.p, h.device, ds->segs.p, ds->device, n * sizeof(uint32_t), ds->stream));
+        if (draws) HIP_TRY(hipMemcpyPeerAsync(m.draws.p, h.device, ds->draws.p, ds->device, n * sizeof(uint32_t), ds->stream));
+        HIP_TRY(hipEventRecord(ds->copy_ev, ds->stream));
+        HIP_TRY(hipSetDevice(h.device));
+        HIP_TRY(hipStreamWaitEvent(h.stream, ds->copy_ev, 0));
+        if (segs) HIP_TRY(launch_add<uint32_t>(h.segs.p, m.segs.p, n, h.stream));
+        if (draws) HIP_TRY(launch_add<uint32_t>(h.draws.p, m.draws.p, n, h.stream));
+    }
+    return RT_OK;
+}
+
 // Peer access between the scene's device and a replica's (hipMemcpyPeerAsync then runs over xGMI
-// directly instead of a staged copy).  Fails loudly if the two devices have no peer path.
+// directly instead of a staged copy).  Without a peer path (PCIe-only topologies, device subsets across
+// root complexes) the copies still work — HIP stages them through host memory — so that is not an
+// error: it is reported once on stderr and the render goes on.  Only an unexpected failure of
+// hipDeviceEnablePeerAccess fails the render.
 int enable_peer(int a, int b) {
     if (a == b) return RT_OK;
     for (int k = 0; k < 2; ++k) {
         const int from = k ? b : a, to = k ? a : b;
         int can = 0;
         HIP_TRY(hipDeviceCanAccessPeer(&can, from, to));
-        if (!can) return fail(RT_ERR_DEVICE, "device %d cannot access device %d (no peer path for the sample split)", from, to);
+        if (!can) {
+            static std::atomic<bool> told{false};
+            if (!told.exchange(true))
+                fprintf(stderr, "[rt_hip] device %d has no peer access to device %d: the sample split's copies are "
+                        "staged through host memory\n", from, to);
+            continue;
+        }
         HIP_TRY(hipSetDevice(from));
         const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
         if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
@@ -587,6 +681,13 @@ int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out) {
     int rc = sc->home.init(device, sc->hs, sc->desc.d);
     hipError_t e = hipSuccess;
     for (int k = 0; k < 2 && !rc && e == hipSuccess; ++k) e = hipEventCreate(&sc->ev[k]);
+    if (!rc && e == hipSuccess)
+        e = hipHostMalloc((void**)&sc->ctl, kCtlWords * sizeof(uint32_t),
+                          hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);
+    if (!rc && e == hipSuccess) {
+        memset(sc->ctl, 0, kCtlWords * sizeof(uint32_t));
+        e = hipHostGetDevicePointer((void**)&sc->ctl_dev, sc->ctl, 0);
+    }
     if (!rc && e != hipSuccess) rc = fail(RT_ERR_DEVICE, "event create: %s", hipGetErrorString(e));
     if (rc) {
         rt_scene_destroy(sc);
@@ -606,13 +707,11 @@ void rt_scene_destroy(rt_scene* sc) {
     sc->home.release();
     (void)hipSetDevice(sc->home.device);
     sc->mean.release(); sc->post.release(); sc->post_raw.release();
-    for (MergeSlot& m : sc->merge) {
-        m.sum.release(); m.segs.release(); m.draws.release();
-        if (m.added) (void)hipEventDestroy(m.added);
-    }
+    for (MergeSlot& m : sc->merge) m.release();
     sc->rgba.release();
     for (uint8_t* p : sc->preview_host)
         if (p) (void)hipHostFree(p);
+    if (sc->ctl) (void)hipHostFree(sc->ctl);
     for (hipEvent_t e : {sc->ev[0], sc->ev[1]})
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : sc->batch_done)
@@ -623,6 +722,7 @@ void rt_scene_destroy(rt_scene* sc) {
 int rt_cancel(rt_scene* sc) {
     if (!sc) return fail(RT_ERR_INVALID, "scene is NULL");
     sc->cancel.store(1);
+    if (sc->ctl) ctl_store(sc->ctl, kCtlCancel, 1);   // the queued batches stop at their next item
     return RT_OK;
 }
 
@@ -684,8 +784,11 @@ int merge_shards(rt_scene* sc, const std::vector<DeviceState*>& states, size_t n
 // batch, consecutive batches also trace on two streams into their own chunk partials (trace_overlapped):
 // the next batch's waves fill the CUs while the previous one drains, and the reduces add the partials in
 // batch order, so the sums are bit-identical to running the batches one after the other (and to a
-// checkpoint + resume at any batch boundary).  A cancel (progress() returning non-zero, rt_cancel) is
-// observed after a batch: the batch already in flight completes and is part of the checkpoint.
+// checkpoint + resume at any batch boundary).  A cancel (progress() returning non-zero, rt_cancel) stops
+// the overlapped batches at their next (tile, chunk) item — a wave's item, about a millisecond — and
+// the checkpoint is the batches fully reduced by then (`gated`); without overlapped batches it is
+// observed after a batch, and the batches already queued complete.  Several devices: whole batches
+// round-robin (trace_replica), or every batch split over the devices (merge_shards).
 int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progress_fn progress, void* user,
                 rt_stats* stats, const double* sums_in, int first) {
     const double t_start = now_ms();
@@ -697,6 +800,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     std::vector<DeviceState*> states;
     if ((rc = shard_states(sc, s, states))) return rc;
     sc->cancel.store(0);
+    ctl_store(sc->ctl, kCtlCancel, 0);
     const size_t n = (size_t)cw * ch;
     const bool want_segs = out && out->segments, want_draws = out && out->draws;
     const bool pool = use_pool(s);
@@ -704,37 +808,69 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     const int base = im.s_begin;                  // the sums hold samples [base, done) of every pixel
     im.s_begin = std::max(im.s_begin, first);
     const int s0 = im.s_begin, s1 = std::max(im.s_end, s0);
-    const int batch = s->batch_samples > 0 ? s->batch_samples : std::max(1, s1 - s0);
-    const int nb = s1 > s0 ? (s1 - s0 + batch - 1) / batch : 0;
     const int nsh = (int)states.size();
     DeviceState& h = sc->home;
+    static const bool overlap_env = !(getenv("RT_OVERLAP") && getenv("RT_OVERLAP")[0] == '0');   // A/B runs
+    // Several devices with the sample pool: whole batches round-robin (batch k on states[k % nsh],
+    // trace_replica), at least one batch per device — the batch size counts from sample_begin, so a
+    // resume at a batch boundary sees the same batches.  Every batch's pool waves take min(batch, chunk)
+    // samples, chunk being the pool's rule for the whole render (as one device's batches do), so the
+    // sums are bit-identical to the same batches on one device.
+    bool whole = nsh > 1 && pool && s->max_depth > 0 && overlap_env && s1 > s0;
+    int whole_batch = 0, whole_chunk = 0;
+    if (whole) {
+        const int full = s->batch_samples > 0 ? s->batch_samples : std::max(1, s1 - base);
+        whole_batch = std::max(1, std::min(full, (s1 - base + nsh - 1) / nsh));
+        whole_chunk = pool_plan(cw, ch, std::max(1, s1 - base), sc->tri_bvh).chunk;
+        const int ns = std::min(whole_batch, s1 - s0);
+        const size_t bytes = pool_plan(cw, ch, ns, sc->tri_bvh, std::min(whole_chunk, ns)).part_bytes;
+        for (int k = 0; k < nsh && whole; ++k) {    // every device's partial slots must fit, else split batches
+            HIP_TRY(hipSetDevice(states[k]->device));
+            whole = ensure_overlap_partials(*states[k], bytes);
+        }
+    }
+    const int batch = whole ? whole_batch : s->batch_samples > 0 ? s->batch_samples : std::max(1, s1 - s0);
+    const int nb = s1 > s0 ? (s1 - s0 + batch - 1) / batch : 0;
     const bool want_preview = out && out->preview_rgba8 && nb > 1;
     std::vector<Counters> cs(nsh);
-    // Several batches: every batch's pool waves take min(batch, chunk) samples, chunk being the pool's
-    // rule for the shard's whole share of the render (not for one batch: short chunks lengthen each
-    // wave's drain relative to its work).  The same batches give the same chunks on a resume (the share
-    // is counted from sample_begin), so a resumed render stays bit-identical.
-    std::vector<int> chunk_hint(nsh, 0);
-    if (pool && nb > 1)
+    // Several batches (split mode): every batch's pool waves take min(batch, chunk) samples, chunk being
+    // the pool's rule for the shard's whole share of the render (not for one batch: short chunks lengthen
+    // each wave's drain relative to its work).  The same batches give the same chunks on a resume (the
+    // share is counted from sample_begin), so a resumed render stays bit-identical.
+    std::vector<int> chunk_hint(nsh, whole ? whole_chunk : 0);
+    if (pool && nb > 1 && !whole)
         for (int k = 0; k < nsh; ++k) {
             int a, b;
             shard_range(base, s1, k, nsh, a, b);
             chunk_hint[k] = pool_plan(cw, ch, std::max(1, b - a), sc->tri_bvh).chunk;
         }
     auto batch_chunk = [&](int k, int ns) { return chunk_hint[k] > 0 ? std::max(1, std::min(chunk_hint[k], ns)) : 0; };
-    // overlapped batches: the pool with several batches.  Not with per-pixel counters over several
-    // devices: the trace kernels add those directly, and a replica's merge zeroes them between batches
-    static const bool overlap_env = !(getenv("RT_OVERLAP") && getenv("RT_OVERLAP")[0] == '0');   // A/B runs
-    bool overlap = overlap_env && pool && nb > 1 && s->max_depth > 0 && !(nsh > 1 && (want_segs || want_draws));
+    // overlapped batches: the pool with several batches (always in whole-batch mode).  Not with per-pixel
+    // counters over a split of every batch: the trace kernels add those directly, and a replica's merge
+    // zeroes them between batches
+    bool overlap = whole || (overlap_env && pool && nb > 1 && s->max_depth > 0 && !(nsh > 1 && (want_segs || want_draws)));
     for (int k = 0; k < nsh; ++k) {
         DeviceState& ds = *states[k];
         HIP_TRY(hipSetDevice(ds.device));
         HIP_TRY(ds.sum.ensure(3 * n));
         HIP_TRY(ds.total.ensure(kTotalSlots));
+        if (whole) continue;
         int b0, b1;
         shard_range(s0, s0 + std::min(batch, s1 - s0), k, nsh, b0, b1);
         const int ns = std::max(1, b1 - b0);
         if (overlap) overlap = ensure_overlap_partials(ds, pool_plan(cw, ch, ns, sc->tri_bvh, batch_chunk(k, ns)).part_bytes);
+    }
+    if (whole && sc->merge.size() < states.size()) sc->merge.resize(states.size());
+    const int ahead = whole ? lookahead(nsh) : kSlots;   // batches queued beyond the one the host waits for
+    const int ring = ahead + kSlots;                      // completion events / preview frames
+    // A cancel inside a batch: the pool kernels read the cancel word before every item, and a batch with
+    // untraced items is never reduced (ReduceGate), nor is any batch after it, so the sums always hold
+    // the batches [0, k) for some k.  For batches reduced on one stream in batch order: one device, or
+    // the whole-batch split.  The split of every batch over devices observes a cancel between batches.
+    const bool gated = overlap && (nsh == 1 || whole);
+    if (gated) {
+        HIP_TRY(hipSetDevice(h.device));
+        HIP_TRY(h.gate_skip.ensure(1));
     }
     for (int k = 0; k < nsh; ++k) {
         DeviceState& ds = *states[k];
@@ -782,16 +918,19 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         }
     }
     HIP_TRY(hipSetDevice(h.device));
+    if ((int)sc->batch_done.size() < ring) sc->batch_done.resize(ring, nullptr);
     for (hipEvent_t& e : sc->batch_done)
         if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (want_preview) {
-        if (sc->preview_host_n < 4 * n) {
+        if (sc->preview_host_n < 4 * n || (int)sc->preview_host.size() < ring) {
             for (uint8_t*& p : sc->preview_host) {
                 if (p) (void)hipHostFree(p);
                 p = nullptr;
             }
             sc->preview_host_n = 0;
-            for (int k = 0; k < kDone; ++k) {
+            sc->preview_host.assign(ring, nullptr);
+            sc->preview_dev.assign(ring, nullptr);
+            for (int k = 0; k < ring; ++k) {
                 HIP_TRY(hipHostMalloc((void**)&sc->preview_host[k], 4 * n, hipHostMallocMapped));
                 HIP_TRY(hipHostGetDevicePointer((void**)&sc->preview_dev[k], sc->preview_host[k], 0));
             }
@@ -800,44 +939,81 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     }
     sc->ckpt_pixels = n;
     sc->ckpt_done = s0;
+    ctl_store(sc->ctl, kCtlStop, 0);
+    ctl_store(sc->ctl, kCtlDone, (uint32_t)s0);
 
     int enqueued = 0;                             // batches [0, enqueued) are queued on the GPU
+    std::vector<unsigned> slots_used(nsh, 0);     // whole-batch split: the partial slots each device traced into
     // enqueue batch kb (no host wait): every shard's trace, the merge of the shards into the home device,
-    // the preview frame, then batch_done[kb % kDone] on the home stream
+    // the preview frame, then batch_done[kb % ring] on the home stream
     auto enqueue = [&](int kb) -> int {
         const int b = s0 + kb * batch, be = std::min(s1, b + batch);
-        for (int k = 0; k < nsh; ++k) {           // every shard's launches first: the devices run together
+        ReduceGate gate;                          // gated: batch kb's cancel and commit words
+        const ReduceGate* gp = nullptr;
+        if (gated) {
+            const int w = kCtlAborted + kb % ring;
+            ctl_store(sc->ctl, w, 0);             // batch kb - ring, the slot's last user, has completed
+            gate.aborted = sc->ctl_dev + w;
+            gate.stop = sc->ctl_dev + kCtlStop;
+            gate.done = reinterpret_cast<int32_t*>(sc->ctl_dev + kCtlDone);
+            gate.done_value = be;
+            gate.skip = h.gate_skip.p;
+            gp = &gate;
+        }
+        auto with_cancel = [&](Counters c) {
+            if (gated) {
+                c.cancel = sc->ctl_dev + kCtlCancel;
+                c.aborted = const_cast<uint32_t*>(gate.aborted);
+            }
+            return c;
+        };
+        if (whole) {                              // the whole batch on one device, reduced on the home device
+            const int k = kb % nsh, lj = kb / nsh, j = lj % kSlots;
+            DeviceState& ds = *states[k];
+            ImageParams bi = im;
+            bi.s_begin = b;
+            bi.s_end = be;
+            bi.pool_chunk = batch_chunk(k, be - b);
+            HIP_TRY(hipSetDevice(ds.device));
+            slots_used[k] |= 1u << j;
+            if (&ds == &h) HIP_TRY(trace_overlapped(sc, ds, s, bi, with_cancel(cs[k]), j, lj >= kSlots, gp));
+            else if (int r = trace_replica(sc, ds, sc->merge[k], s, bi, with_cancel(cs[k]), j, gp)) return r;
+        }
+        for (int k = 0; k < nsh && !whole; ++k) { // every shard's launches first: the devices run together
             DeviceState& ds = *states[k];
             ImageParams bi = im;
             shard_range(b, be, k, nsh, bi.s_begin, bi.s_end);
             bi.pool_chunk = batch_chunk(k, bi.s_end - bi.s_begin);
             HIP_TRY(hipSetDevice(ds.device));
-            if (overlap) HIP_TRY(trace_overlapped(sc, ds, s, bi, cs[k], kb % kSlots, kb >= kSlots));
+            if (overlap) HIP_TRY(trace_overlapped(sc, ds, s, bi, with_cancel(cs[k]), kb % kSlots, kb >= kSlots, gp));
             else HIP_TRY(trace(sc, ds, s, bi, cs[k], ds.stream));
         }
         int r;
-        if (nsh > 1 && (r = merge_shards(sc, states, n, want_segs, want_draws))) return r;
+        if (nsh > 1 && !whole && (r = merge_shards(sc, states, n, want_segs, want_draws))) return r;
         HIP_TRY(hipSetDevice(h.device));
         if (want_preview && be < s1) {            // the running frame: mean over the samples so far
             // written by the epilogue kernel straight into pinned host memory (over PCIe): a
             // hipMemcpyAsync here is a blit kernel that waits for wave slots behind the trace waves
             // (measured 7-15 ms per 8-MB frame while batches overlap)
             FinalizeParams fp{(int)n, be - base, s->tone_map, s->exposure, s->gamma};
-            HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview_dev[kb % kDone], h.stream));
+            HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview_dev[kb % ring], h.stream));
         }
-        HIP_TRY(hipEventRecord(sc->batch_done[kb % kDone], h.stream));
+        HIP_TRY(hipEventRecord(sc->batch_done[kb % ring], h.stream));
         return RT_OK;
     };
-    // host side of batch kb once batch_done: checkpoint state and the preview frame
-    auto complete = [&](int kb) -> int {
-        HIP_TRY(hipEventSynchronize(sc->batch_done[kb % kDone]));
+    // host side of batch kb once batch_done: checkpoint state and the preview frame.  merged: the batch
+    // is in the sums (gated renders: not if a cancel left it unfinished)
+    auto complete = [&](int kb, bool& merged) -> int {
+        HIP_TRY(hipEventSynchronize(sc->batch_done[kb % ring]));
         const int be = std::min(s1, s0 + (kb + 1) * batch);
+        merged = !gated || (int)ctl_load(sc->ctl, kCtlDone) >= be;
+        if (!merged) return RT_OK;
         sc->ckpt_done = be;
         // the running frame, unless the next batch has finished too (its frame supersedes this one: the
         // host does not fall further behind the GPU copying frames nobody will see)
         if (want_preview && be < s1 &&
-            !(kb + 1 < enqueued && hipEventQuery(sc->batch_done[(kb + 1) % kDone]) == hipSuccess)) {
-            memcpy(out->preview_rgba8, sc->preview_host[kb % kDone], 4 * n);
+            !(kb + 1 < enqueued && hipEventQuery(sc->batch_done[(kb + 1) % ring]) == hipSuccess)) {
+            memcpy(out->preview_rgba8, sc->preview_host[kb % ring], 4 * n);
             if (out->preview_samples) *out->preview_samples = be - base;
         }
         return RT_OK;
@@ -854,13 +1030,34 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         return RT_OK;
     };
     for (int kb = 0; kb < nb && status == RT_OK; ++kb) {
-        if ((status = fill(kb + kSlots + 1))) break;
-        if ((status = complete(kb))) break;
+        if ((status = fill(kb + ahead + 1))) break;
+        bool merged = true;
+        if ((status = complete(kb, merged))) break;
         const int be = sc->ckpt_done;
-        if (progress && be < s1 && progress((double)(be - s0) / (double)(s1 - s0), user)) sc->cancel.store(1);
-        if (sc->cancel.load()) {
-            // the batches in flight finish (and if the last one was among them, the render completed)
-            for (int k = kb + 1; k < enqueued && status == RT_OK; ++k) status = complete(k);
+        if (merged && progress && be < s1 && progress((double)(be - s0) / (double)(s1 - s0), user)) {
+            sc->cancel.store(1);
+            ctl_store(sc->ctl, kCtlCancel, 1);
+        }
+        if (!merged || sc->cancel.load()) {
+            if (gated) {
+                // the queued batches stop at their next item and are not reduced; once every stream has
+                // drained, the sums hold exactly the batches the gates committed
+                ctl_store(sc->ctl, kCtlCancel, 1);
+                for (DeviceState* ds : states) ds->sync_all();
+                h.sync_all();
+                sc->ckpt_done = (int)ctl_load(sc->ctl, kCtlDone);
+                if (want_preview && sc->ckpt_done > base && sc->ckpt_done < s1) {   // the checkpoint's frame
+                    HIP_TRY(hipSetDevice(h.device));
+                    FinalizeParams fp{(int)n, sc->ckpt_done - base, s->tone_map, s->exposure, s->gamma};
+                    HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview_dev[0], h.stream));
+                    HIP_TRY(hipStreamSynchronize(h.stream));
+                    memcpy(out->preview_rgba8, sc->preview_host[0], 4 * n);
+                    if (out->preview_samples) *out->preview_samples = sc->ckpt_done - base;
+                }
+            } else {
+                // the batches in flight finish (and if the last one was among them, the render completed)
+                for (int k = kb + 1; k < enqueued && status == RT_OK; ++k) status = complete(k, merged);
+            }
             if (status == RT_OK && sc->ckpt_done < s1)
                 status = fail(RT_ERR_CANCELLED, "render cancelled after %d samples", sc->ckpt_done);
             break;
@@ -878,6 +1075,15 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         (void)hipGetLastError();
         g_error = err;
         return status;
+    }
+    if (whole) {   // every device's accumulation stream after its trace streams; the replicas' counters
+        for (int k = 0; k < nsh; ++k) {
+            DeviceState* ds = states[k];
+            HIP_TRY(hipSetDevice(ds->device));
+            for (int j = 0; j < kSlots; ++j)
+                if (slots_used[k] & (1u << j)) HIP_TRY(hipStreamWaitEvent(ds->stream, ds->traced[j], 0));
+        }
+        if ((rc = merge_counters(sc, states, n, want_segs, want_draws))) return rc;
     }
     unsigned long long totals[kTotalSlots] = {};
     float kernel_ms = 0;

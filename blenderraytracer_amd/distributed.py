@@ -21,8 +21,10 @@ def sample_range(rank, world, samples):
 
 
 def reduce_sums(buf, world, group=None):
-    """Sum the per-pixel radiance sums of all ranks into rank 0's buffer (RCCL reduce on GPUs)."""
-    if world > 1:
+    """Sum the per-pixel radiance sums of all ranks into rank 0's buffer (RCCL reduce on GPUs).  Runs
+    whenever a process group is up, also at world size 1 (bench.py under torch.distributed.run with one
+    rank: the RCCL path itself, an identity there)."""
+    if world > 1 or (dist.is_available() and dist.is_initialized()):
         if buf.is_cuda and dist.get_backend(group) == "gloo":
             # gloo reduces host tensors only: the N-ranks-on-fewer-GPUs rehearsal (bench.py
             # --dist-backend gloo) stages the sums through host memory
@@ -67,15 +69,21 @@ class ShardedRender:
                                             C.c_void_p(stream.cuda_stream), 1 if stats else 0,
                                             C.byref(self.stats) if stats else None))
 
-    def step(self, stats=True):
+    def step(self, stats=True, events=None):
         """Render the frame once.  With stats=True (HIP path) the trace kernel's HIP-event time and
-        segment count land in self.stats (the call then synchronizes the stream after the trace)."""
+        segment count land in self.stats (the call then synchronizes the stream after the trace).
+        events: (start, end) torch.cuda.Events recorded around the trace on the stream it runs on (the
+        timed steps of bench.py: no host synchronization inside a step)."""
         self.sum.zero_()
         if self.settings is not None:
             if self._trace is not None:
                 self._trace(self.sum, self.settings)
             else:
+                if events:
+                    events[0].record()
                 self._hip_trace(stats)
+                if events:
+                    events[1].record()
         reduce_sums(self.sum, self.world, self.group)
         if self.rank == 0 and self._trace is None:
             stream = torch.cuda.current_stream(self.device)
@@ -86,26 +94,43 @@ class ShardedRender:
 
 class InProcessRender:
     """The drop-in's own multi-GPU path (rt_settings.devices, what installGpuRender(rt, {devices}) runs
-    from Node): ONE process, every frame's samples split into len(devices) contiguous ranges, range k
-    traced on devices[k] by a replica of the scene, the float64 sums copied peer-to-peer over xGMI to
-    the scene's device and added in range order there, then the epilogue.  A step is one rt_render
-    call delivering the frame's RGBA8 bytes to the host (the reference's imageData)."""
+    from Node): ONE process, whole sample batches dealt round-robin to the devices (batch k on
+    devices[k % N], traced by a replica of the scene), each batch's chunk partials copied peer-to-peer
+    over xGMI to the scene's device and added there in batch order, then the epilogue.  A step is one
+    rt_render call delivering the frame's RGBA8 bytes to the host (the reference's imageData).
+    progress_steps: the Node drop-in's progressive form (gpu-ray-tracer.mjs DEFAULT_PROGRESS_STEPS = 16):
+    batches of ceil(samples / steps), the running frame into a preview buffer and a progress callback
+    after every batch; 0: batch_samples = 0 (the library then makes one batch per device)."""
 
-    def __init__(self, tracer, devices):
+    def __init__(self, tracer, devices, progress_steps=0):
         import numpy as np
         self.tracer = tracer
         self.devices = list(devices)
         self.lib = capi.load_library()
         self.scene = tracer.scene_handle()
-        self.settings = tracer.settings(devices=self.devices if len(self.devices) > 1 else None)
+        spp = tracer.settings().samples
+        self.batch = -(-spp // progress_steps) if progress_steps else 0
+        self.settings = tracer.settings(devices=self.devices if len(self.devices) > 1 else None,
+                                        batch_samples=self.batch)
         s = self.settings
         self.n = (s.crop_w or s.width) * (s.crop_h or s.height)
         self.rgba8 = np.zeros(self.n * 4, dtype=np.uint8)
         self.out = capi.Output()
         self.out.rgba8 = self.rgba8.ctypes.data_as(C.POINTER(C.c_uint8))
+        self.progress_calls = 0
+        if progress_steps:
+            self.preview = np.zeros(self.n * 4, dtype=np.uint8)
+            self.out.preview_rgba8 = self.preview.ctypes.data_as(C.POINTER(C.c_uint8))
+
+            def on_progress(fraction, user):
+                self.progress_calls += 1
+                return 0
+            self._progress = capi.PROGRESS_FN(on_progress)
+        else:
+            self._progress = C.cast(None, capi.PROGRESS_FN)
         self.stats = capi.Stats()
         self.range = (0, s.samples)
 
-    def step(self, stats=True):
-        capi.check(self.lib.rt_render(self.scene, C.byref(self.settings), C.byref(self.out), C.cast(None, capi.PROGRESS_FN), None,
+    def step(self, stats=True, events=None):
+        capi.check(self.lib.rt_render(self.scene, C.byref(self.settings), C.byref(self.out), self._progress, None,
                                       C.byref(self.stats)))

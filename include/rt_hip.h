@@ -35,7 +35,7 @@ typedef enum rt_status {
     RT_ERR_INVALID = -1,     /* bad argument / descriptor */
     RT_ERR_DEVICE = -2,      /* HIP runtime error */
     RT_ERR_NOMEM = -3,
-    RT_ERR_CANCELLED = -4,   /* rt_cancel() was observed between sample batches */
+    RT_ERR_CANCELLED = -4,   /* rt_cancel() / progress() stopped the render before its last sample */
     RT_ERR_NO_DEVICE = -5    /* no HIP device visible: the backend never falls back to the CPU */
 } rt_status;
 
@@ -158,16 +158,23 @@ typedef struct rt_settings {
     double denoise_weights[2]; /* Math.exp(-1/(2s*s)), Math.exp(-2/(2s*s)), s = denoiseStrength, evaluated by
                                   the host with its own exp (post-processor.js:55) */
     int32_t accel;             /* rt_accel: how World.hit is evaluated (results are identical) */
-    int32_t device_count;      /* 0 or 1: the scene's own device.  N in 2..RT_MAX_DEVICES: every sample
-                                  batch is split into N contiguous sample ranges, range k traced on HIP
-                                  device devices[k], the per-pixel float64 sums added on the
-                                  scene's device in range order (peer copies over xGMI), then the epilogue.
-                                  A device may be listed more than once (its ranges run on separate
-                                  streams).  The scene is uploaded to each listed device on first use and
-                                  kept.  Equal to one device up to the order of the binary64 additions. */
-    int32_t devices[8];        /* HIP ordinals of the devices (device_count of them); distinct devices need
-                                  peer access to the scene's device (enabled by the library, else
-                                  RT_ERR_DEVICE) */
+    int32_t device_count;      /* 0 or 1: the scene's own device.  N in 2..RT_MAX_DEVICES:
+                                  with the sample pool (sum_order RT_SUM_POOL), WHOLE sample batches are
+                                  dealt round-robin — batch k traced on devices[k % N] — and each batch's
+                                  chunk partials are copied to the scene's device and added there in
+                                  batch order, so the sums are bit-identical to the same batches on one
+                                  device (checkpoint/resume unchanged).  The batch size is then
+                                  min(batch_samples, ceil((samples - sample_begin) / N)) so that every
+                                  device gets work; batch_samples = 0 gives N batches.  With
+                                  RT_SUM_SAMPLE_ORDER (or when the partial slots do not fit) every batch is
+                                  instead split into N contiguous sample ranges, range k on devices[k],
+                                  their sums added on the scene's device in range order (equal to one
+                                  device up to the order of those additions).  A device may be listed more
+                                  than once (its batches run on separate streams).  The scene is uploaded
+                                  to each listed device on first use and kept. */
+    int32_t devices[8];        /* HIP ordinals of the devices (device_count of them).  Peer access to the
+                                  scene's device is enabled where the topology has it; without it the
+                                  copies are staged through host memory (reported once on stderr) */
     int32_t sum_order;         /* rt_sum_order */
 } rt_settings;
 
@@ -184,8 +191,7 @@ typedef struct rt_output {
                                  more than one sample batch, before every progress() call this buffer holds
                                  the RGBA8 frame of the samples traced so far (mean over those samples, tone
                                  map, gamma; no denoise, like the reference's rows before its final pass).
-                                 A cancel is observed after a batch, the batch already in flight completes,
-                                 and the buffer then holds the frame of the checkpointed samples.  A batch
+                                 After a cancel the buffer holds the frame of the checkpointed samples.  A batch
                                  whose successor has already finished when the host gets to it is skipped
                                  (the buffer keeps the previous frame until the newer one is copied) */
     int32_t* preview_samples; /* optional out: the samples (from sample_begin) in preview_rgba8's frame,
@@ -193,7 +199,10 @@ typedef struct rt_output {
 } rt_output;
 
 typedef struct rt_stats {
-    double kernel_ms;            /* device time of the path-tracing launches (HIP events) */
+    double kernel_ms;            /* device time of the path-tracing launches (HIP events on the device's
+                                    accumulation stream, from the render's set-up to its last batch's
+                                    merge; the maximum over devices).  With several batches and a
+                                    progress callback this includes any time the GPU waited for the host */
     double finalize_ms;          /* device time of the epilogue */
     double wall_ms;              /* host wall time of the call */
     uint64_t samples;            /* pixels x samples traced */
@@ -222,9 +231,13 @@ void rt_scene_destroy(rt_scene* scene);
 /* Full render into host buffers: trace, finalize (tone map, gamma, RGBA8) and copy back.
  * Replaces RayTracer.render (ray-tracer.js:166-281) minus the DOM. Synchronous.
  * progress(fraction, user) is called between sample batches from the calling thread; a non-zero
- * return value cancels (like window.renderCancelled, ray-tracer.js:190,196).  Batches are pipelined
- * (the next one is queued on the GPU before the host waits for the current one), so a cancel takes
- * effect after the batch in flight; RT_ERR_CANCELLED unless that was the last batch.
+ * return value cancels (like window.renderCancelled, ray-tracer.js:190,196), as does rt_cancel from any
+ * thread.  Batches are pipelined (up to 3 per device are queued on the GPU beyond the one the host waits
+ * for).  With the sample pool and several batches a cancel stops every queued batch at its next 8x8
+ * tile x sample-chunk item (about a millisecond on config 3) and the render returns once the GPU has
+ * drained; the checkpoint holds the batches fully added before that.  Otherwise (sample order, one
+ * batch, partials that do not fit) it is observed between batches and the queued ones complete.
+ * RT_ERR_CANCELLED unless every sample was traced.
  * Threading: one call in flight per scene (rt_render, rt_render_resume, rt_trace_device,
  * rt_finalize_device, rt_render_checkpoint), as for the reference's render(); calls on different
  * scenes may run concurrently from different threads.  Asynchronous device calls on different streams
@@ -235,7 +248,7 @@ int rt_render(rt_scene* scene, const rt_settings* settings, const rt_output* out
 
 /* Progressive rendering (the reference's row-by-row progress, ray-tracer.js:258-261,
  * at sample granularity).  After rt_render / rt_render_resume returns — finished or cancelled
- * between sample batches (RT_ERR_CANCELLED) — the scene holds the per-pixel float64 radiance sums
+ * (RT_ERR_CANCELLED; the checkpoint is always a whole number of batches) — the scene holds the per-pixel float64 radiance sums
  * of samples [sample_begin, samples_done).  rt_render_checkpoint copies them out (count must be
  * 3 x crop pixels) so a host can persist them; rt_render_resume traces samples
  * [samples_done, sample_end) on top of such sums and finishes like rt_render.  Every pixel still
@@ -274,7 +287,8 @@ int rt_closest_hits(rt_scene* scene, int32_t precision, int32_t accel, const dou
  * walk finds the same closest hit; they differ in speed only. */
 int rt_scene_walk(rt_scene* scene, int32_t precision, int32_t accel);
 
-/* Request cancellation of an in-flight rt_render on `scene` (polled between sample batches). */
+/* Request cancellation of an in-flight rt_render on `scene` (the pool kernels read it before every item;
+ * see rt_render). */
 int rt_cancel(rt_scene* scene);
 
 #ifdef __cplusplus

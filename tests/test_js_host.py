@@ -157,10 +157,11 @@ def test_js_gpu_render_matches_reference(gpu):
         assert r["progress"][-1] == 1.0 and r["nonzero"]
         assert summary["_floatData"] == {"absentByDefault": True, "kept": True, "rgbaEqual": True}
         # window.renderCancelled set in the 2nd of 8 progress callbacks (the addon runs each callback
-        # before the render goes on), the three batches in flight finish, then GpuRayTracer.resume():
-        # the same image as the uninterrupted render
+        # before the render goes on): the batches queued stop at their next item, the checkpoint holds
+        # the batches reduced before that (2 to 5 of them), then GpuRayTracer.resume(): the same image as
+        # the uninterrupted render
         assert summary["_resume"]["equal"] is True
-        assert summary["_resume"]["samplesDone"] == 10
+        assert summary["_resume"]["samplesDone"] in (4, 6, 8, 10), summary["_resume"]
         dv = summary["_devices"]                    # settings.devices = [0, 0] through N-API
         assert dv["segsEqual"] and dv["drawsEqual"] and dv["maxRel"] <= 1e-13, dv
         assert dv["sceneCached"] and dv["reuploaded"], dv
@@ -168,7 +169,12 @@ def test_js_gpu_render_matches_reference(gpu):
         assert len(pg["progress"]) >= 16 and pg["progress"][-1] == 1.0, pg["progress"]
         assert all(x < y for x, y in zip(pg["progress"], pg["progress"][1:])), pg["progress"]
         assert pg["distinctFrames"] >= 2 and pg["lastFrameFinal"], pg
-        assert pg["cancelDone"] == 16 and pg["cancelFrameEqual"], pg
+        assert pg["cancelDone"] in (10, 12, 14, 16) and pg["cancelFrameEqual"], pg
+        # cancel-to-return within one batch: before, the three queued batches ran on
+        cl = summary["_cancelLatency"]
+        print(f"Node cancel-to-return {cl['latencyMs']:.2f} ms, frame {cl['frameMs']:.1f} ms, "
+              f"checkpoint {cl['samplesDone']} of 512 samples")
+        assert cl["latencyMs"] < cl["frameMs"] / 4 and cl["samplesDone"] in (128, 256, 384), cl
 
 
 def test_pow5_vs_v8_math_pow(tmp_path):
