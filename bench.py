@@ -176,6 +176,68 @@ SQ_COUNTERS = ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CY
                "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")
 
 
+# Instruction-floor model: the VALU issue slots per segment that the
+# reference's arithmetic needs (wave64 binary32 / integer VALU instruction = 1 slot, binary64 = 2, as
+# VALU_ISSUE_PEAK_GSLOTS counts them), from the events the kernel's own code performs per segment (counted
+# on the CPU, tests/hostcheck RT_HCOUNT) and a per-event cost in gfx950 instructions: binary64 sqrt =
+# the 20-instruction v_rsq_f64 + Newton expansion (~32 slots), binary64 division = v_div_scale x2 /
+# v_rcp / 5 FMA / v_div_fmas / v_div_fixup (~22 slots).  Addressing, loop control and lane bookkeeping
+# are not counted: this is the arithmetic floor, at lane utilization 1.
+FLOOR_COST = {
+    "walk_step_grid": 12,       # 3D-DDA cell step, binary32 (pt_core.h closest_hit_grid)
+    "walk_step_bvh": 24,        # two-child node: 6 packed FMA slab planes + min/max + child choice (binary32)
+    "filter_tests": 12,         # binary32 sphere pre-filter (pt_core.h sphere_filter_pass)
+    "f64_sphere_tests": 36,     # oc, halfB, c, discriminant: 17 binary64 ops + compare (geometry.js:16-22)
+    "disc_nonneg": 58,          # sqrt + (-halfB - sqrtd) / a + tMin test (geometry.js:24-26)
+    "second_root": 26,          # (-halfB + sqrtd) / a + test (geometry.js:27-28)
+    "tri_tests": 102,           # Moller-Trumbore: 2 cross, 4 dot, 1 division (geometry.js:148-188)
+    "plane_tests": 50,          # dot, (p - o).n / denom (geometry.js:56-74)
+    "box_tests": 150,           # six divisions + slab logic (geometry.js:85-117)
+    "hit": 100,                 # ray.at(t), (p - c) / radius (3 divisions), setFaceNormal (math.js:41,55-58)
+    "segment": 108,             # one normalize per segment: length (sqrt) + 3 divisions (math.js:18)
+    "lambertian": 12,           # n + unit, attenuation (materials.js:20-25)
+    "metal": 54,                # reflect + fuzz * p + dot test (materials.js:36-41)
+    "dielectric": 118,          # ratio, cos, sin (sqrt), refract/reflect (materials.js:51-83)
+    "dielectric_schlick": 68,   # r0, pow5 (10 binary64 ops), draw and compare (materials.js:79-83)
+    "emissive": 6,              # emission x throughput (materials.js:87-96)
+    "miss": 34,                 # skyGradient x intensity x throughput (world.js:35-44)
+    "sphere_draw_rounds": 45,   # 3 keyed draws + integer |p|^2 < 1 test (math.js:22-26)
+    "disk_draw_rounds": 30,     # 2 keyed draws + integer test (math.js:27-31)
+    "samples": 151,             # sample key, 2 AA draws, (i + r) / width x 2, camera ray (camera.js:38-51)
+}
+
+
+def instruction_floor(rt, cfg, side=32, spp=8):
+    """The instruction floor of the workload (FLOOR_COST over the kernel's events per segment on three
+    crops of the frame at `spp`, counted on the CPU by the kernel's own code)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes
+    import hostcheck_binding as hb
+    packed = rt.packed()
+    n3, regs, use_grid = (ctypes.c_int * 3)(), ctypes.c_longlong(), ctypes.c_int()
+    hb.lib().ptc_grid_info(ctypes.byref(packed.desc), n3, ctypes.byref(regs), ctypes.byref(use_grid))
+    prims = sum(o.count if k in ("mesh", "triangle") else 1 if k == "sphere" else 0
+                for k, o in zip(packed.kinds, packed.objects))
+    walk = "grid" if use_grid.value else ("bvh" if prims >= 8 else "brute")
+    w, h = cfg["w"], cfg["h"]
+    sts = []
+    for fx, fy in ((0.5, 0.5), (0.25, 0.7), (0.75, 0.3)):
+        st = rt.settings(crop=(int(fx * (w - side)), int(fy * (h - side)), side, side))
+        st.samples = spp
+        sts.append(st)
+    ev = hb.event_counts(packed, sts, walk)
+    ev["plane_tests"] = float(sum(1 for k in packed.kinds if k == "plane"))
+    ev["box_tests"] = float(sum(1 for k in packed.kinds if k == "box"))
+    ev["hit"] = 1.0 - ev["miss"]
+    ev["segment"] = 1.0
+    ev["walk_step_" + ("grid" if walk == "grid" else "bvh")] = ev["walk_steps"] if walk != "brute" else 0.0
+    slots = {k: FLOOR_COST[k] * ev.get(k, 0.0) for k in FLOOR_COST}
+    return {"walk": walk, "events_per_segment": {k: round(v, 4) for k, v in ev.items()},
+            "lane_slots_per_segment": round(sum(slots.values()), 1),
+            "lane_slots_by_event": {k: round(v, 1) for k, v in slots.items() if v},
+            "sample": f"3 crops of {side}x{side} at {spp} spp, the kernel's code on the CPU (tests/hostcheck RT_HCOUNT)"}
+
+
 def pmc_child(args):
     """--pmc-child: one frame of the workload through rt_render (the same trace launches as a bench
     step), run under rocprofv3 --pmc by pmc_passes()."""
@@ -492,6 +554,20 @@ def main():
                                           "rocprofv3's GRBM_GUI_ACTIVE is the sum over the 8 XCDs "
                                           "(MI355X_MICROARCH.md); l1_hit = 1 - TCP_TCC_READ_REQ / TCP accesses",
                             "source": "rocprofv3 --pmc pass over one frame run by this bench invocation"}
+        floor = None
+        if args.gpus == 1:
+            try:
+                floor = instruction_floor(rt, cfg)
+                fl_ms = seg_launch * floor["lane_slots_per_segment"] / 64.0 / (VALU_ISSUE_PEAK_GSLOTS * 1e9) * 1e3
+                floor.update({"floor_ms": round(fl_ms, 3), "kernel_ms": round(k_ms, 3), "frac": round(fl_ms / k_ms, 4),
+                              "peak": VALU_ISSUE_PEAK_GSLOTS, "unit": "G issue slots/s at lane utilization 1",
+                              "definition": "the reference arithmetic's VALU issue slots (FLOOR_COST x the kernel's "
+                                            "events per segment) x this frame's segments / 64 lanes / peak; frac = "
+                                            "floor_ms / the measured trace-step time"})
+            except Exception as e:      # the host-check library is test infrastructure: report, do not fail
+                floor = {"error": f"{type(e).__name__}: {e}"}
+            if binding is not None:
+                binding["floor"] = floor
         roofline.update({
             "cache_served_bytes": a_bytes,
             "cache_served_GBps": round(a_bytes / (k_ms * 1e-3) / 1e9, 2),
@@ -534,7 +610,7 @@ def main():
             "mp_mode": mp_mode,
             "progressive_16": progressive,
             "roofline": roofline,
-            "roofline_binding": binding,
+            "roofline_binding": binding if binding is not None else ({"floor": floor} if floor else None),
             "roofline_vmem": vmem,
             "valu_flops": {"achieved": round(flops / (k_ms * 1e-3) / 1e12, 3), "peak": VALU_PEAK_TFLOPS[args.precision],
                            "unit": "TFLOP/s", "frac": round(flops / (k_ms * 1e-3) / 1e12 / VALU_PEAK_TFLOPS[args.precision], 4),

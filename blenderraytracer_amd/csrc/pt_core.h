@@ -29,6 +29,18 @@
 
 namespace rt {
 
+// Host-only event counts for the instruction-floor model: compiled into the host check
+// built with -DRT_HOST_COUNTERS (scripts/floor_counts.py) and nowhere else.
+#if defined(RT_HOST_COUNTERS) && !defined(__HIP_DEVICE_COMPILE__)
+extern unsigned long long rt_host_count[16];
+#define RT_HCOUNT(k, n) (rt_host_count[k] += (n))
+#else
+#define RT_HCOUNT(k, n) ((void)0)
+#endif
+enum HostCount { HC_F64_TESTS = 0, HC_DISC_OK, HC_SECOND_ROOT, HC_ACCEPT, HC_LAMBERT, HC_METAL, HC_DIELECTRIC,
+                 HC_EMISSIVE, HC_MISS, HC_SAMPLES, HC_SPHERE_DRAW_ROUNDS, HC_DISK_DRAW_ROUNDS, HC_FILTER_TESTS,
+                 HC_DIELECTRIC_SCHLICK };
+
 // ---- keyed RNG ------------------------------------------------------------------
 RT_HD uint32_t lowbias32(uint32_t x) {
     x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16; return x;
@@ -245,6 +257,7 @@ RT_HD FilterRay make_filter_ray(V3<R> o, V3<R> d) {
 
 // false only if the sphere is certainly missed in binary64 (disc64 < 0): 12 VALU per sphere
 RT_HD bool sphere_filter_pass(const SphereFilter& s, const FilterRay& r) {
+    RT_HCOUNT(HC_FILTER_TESTS, 1);
     const float ocx = r.ox - s.cx, ocy = r.oy - s.cy, ocz = r.oz - s.cz;
     const float hb = __builtin_fmaf(ocx, r.dx, __builtin_fmaf(ocy, r.dy, ocz * r.dz));
     const float cc = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, __builtin_fmaf(ocz, ocz, -(s.r2p + r.delta))));
@@ -354,15 +367,18 @@ RT_HD bool better(R t, int obj, int id, const Closest<R>& b) {
 // ray leaving them (the RTOW ground: most secondary rays) would otherwise test in full: +0.9 %.
 template <class R>
 RT_HD bool sphere_candidate(const SphereRec<R>& s, V3<R> o, V3<R> d, R a, R tmin, R& t, bool away = false) {   // geometry.js:15-45
+    RT_HCOUNT(HC_F64_TESTS, 1);
     R ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
     R hb = ocx * d.x + ocy * d.y + ocz * d.z;
     R c = (ocx * ocx + ocy * ocy + ocz * ocz) - s.r2;
     if (away && c >= (R)0 && hb >= (R)0) return false;
     R disc = hb * hb - a * c;
     if (disc < (R)0) return false;
+    RT_HCOUNT(HC_DISC_OK, 1);
     R sq = sqrt(disc);
     t = (-hb - sq) / a;
     if (!(t < tmin)) return true;
+    RT_HCOUNT(HC_SECOND_ROOT, 1);
     t = (-hb + sq) / a;
     return !(t < tmin);
 }
@@ -711,7 +727,8 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
 // interval lies within e <= 2^-19 (|o|_inf + B) of that cell (B: the grid's coordinate bound; binary32
 // origin, boundary and product roundings, approximate reciprocal), so any sphere hit at t' <= T in
 // binary64 is registered in a cell already walked when m >= e: build_grid sets m = 2^-12 (B + extent)
-// and grid_far = 2^7 (B + extent) bounds |o|_inf, so e <= 2^-12 (B + extent) (rays from farther away
+// and grid_far = 2^6 (B + extent) bounds |o|_inf, so e <= 2^-19 (2^6 + 1) (B + extent) < m
+// (scene_pack.h kGridMargin / kGridFar, static_assert there) (rays from farther away
 // test every sphere).  The walk stops when the best t is below the current cell's exit, so a sphere
 // reaching the best t exactly (a tie that World.hit's order decides) is still tested.  The closest hit
 // is therefore World.hit's, as for the BVH (tests/test_hostcheck.py, tests/test_gpu_parity.py).
@@ -726,10 +743,42 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
 // Grid records [first, end) read from their LDS copy (ACC_GRID_LDS): binary64 tests the binary32 filter
 // from LDS and reads the rest of the record from recs only when it passes; binary32 reads the whole
 // record from LDS.  The same tests in the same order as sphere_records: same hits, same bits.
+// RT_GRID_COMPACT (binary64): a cell's records are filtered first, 32 at a time, into a per-lane mask of
+// survivors, and the binary64 tests then run over each lane's survivors: lanes whose survivors sit at
+// different positions of their cells run the binary64 test together instead of each in its own record
+// iteration.  The order of the tests within a cell does not matter (`better` is a total order).
+#ifndef RT_GRID_COMPACT
+#define RT_GRID_COMPACT 1
+#endif
 template <class R>
 RT_HD void sphere_records_lds(const rt_u4* lrec, const SphereLeaf<R>* recs, int first, int end, V3<R> o, V3<R> d,
                               R a, const FilterRay& fr, R tmin, Closest<R>& b, float& tl, Work& w) {
     RT_COUNT(w.spheres += end - first);
+    if constexpr (sizeof(R) == 8 && RT_GRID_COMPACT != 0) {
+        for (int base = first; base < end; base += 32) {
+            const int n = end - base < 32 ? end - base : 32;
+            uint32_t pass = 0;
+            for (int i = 0; i < n; ++i) {
+                const rt_u4 q = lrec[base + i];
+                SphereFilter f;
+                memcpy(&f, &q, sizeof f);
+                if (sphere_filter_pass(f, fr)) pass |= 1u << i;
+            }
+            while (pass) {
+                const int k = base + __builtin_ctz(pass);
+                pass &= pass - 1;
+                const SphereRec<R> s = recs[k].s;
+                const int id = recs[k].id, obj = recs[k].obj, mat = recs[k].mat;
+                R t;
+                if (!sphere_candidate(s, o, d, a, tmin, t)) continue;
+                if (better(t, obj, id, b)) {
+                    b = Closest<R>{t, HIT_SPHERE, id, mat, obj};
+                    tl = bvh_tlimit(b.t);
+                }
+            }
+        }
+        return;
+    }
     for (int k = first; k < end; ++k) {
         SphereRec<R> s;
         int id, obj, mat;
@@ -913,6 +962,7 @@ RT_HD V3<R> random_in_unit_sphere(Rng<R>& g) {                  // math.js:22-26
     // decisions at integer cost (and the exact decision in f32 mode too).
     int64_t x, y, z;
     do {
+        RT_HCOUNT(HC_SPHERE_DRAW_ROUNDS, 1);
         x = (int64_t)g.next_u24() - (1 << 23);
         y = (int64_t)g.next_u24() - (1 << 23);
         z = (int64_t)g.next_u24() - (1 << 23);
@@ -924,6 +974,7 @@ template <class R>
 RT_HD V3<R> random_in_unit_disk(Rng<R>& g) {                    // math.js:27-31
     int64_t x, y;                                                 // exact, as random_in_unit_sphere
     do {
+        RT_HCOUNT(HC_DISK_DRAW_ROUNDS, 1);
         x = (int64_t)g.next_u24() - (1 << 23);
         y = (int64_t)g.next_u24() - (1 << 23);
     } while (x * x + y * y >= ((int64_t)1 << 46));

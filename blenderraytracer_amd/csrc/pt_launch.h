@@ -24,10 +24,13 @@ struct Counters {
     size_t part_bytes = 0;
     // progressive renders (render_impl): the render's cancel word in mapped host memory, read by the pool
     // kernels before every (tile, chunk) item; a wave that finds it set leaves its items untraced and
-    // sets *aborted (this batch's word, mapped host memory too), so that the batch is never reduced
+    // sets *aborted (this batch's word, mapped host memory too), so that the batch is never reduced.
+    // kCancelCopies copies of the word, one per 128-B line (cancel[k * kCancelStride]), the host writes
+    // all of them: the waves' reads spread over many lines instead of queueing on one
     const uint32_t* cancel = nullptr;
     uint32_t* aborted = nullptr;
 };
+constexpr int kCancelCopies = 128, kCancelStride = 32;
 
 // The commit of one batch's chunk partials (render_impl with a cancel word): a one-thread gate kernel
 // before the reduce reads the batch's `aborted` word and the render's sticky `stop` word (both mapped

@@ -39,6 +39,7 @@ RT_COLD_HD AaUv<R> stochastic_uv(uint32_t key, int i, int j, int width, int heig
 template <class R>
 RT_HD void start_sample(const SceneView<R>& sc, const ImageParams& im, int i, int j, uint32_t pkey, int s, Rng<R>& g,
                         V3<R>& o, V3<R>& d) {
+    RT_HCOUNT(HC_SAMPLES, 1);
     g.key = sample_key(pkey, (uint32_t)s);
     g.k = 0;
     R u, v;                                                                   // ray-tracer.js:125-149
@@ -103,17 +104,21 @@ RT_HD bool scatter(const MatRec<R>& m, const Hit<R>& h, V3<R> unit, V3<R> p, Rng
     if (m.type <= 1) {
         att = mk(m.c[0], m.c[1], m.c[2]);
         if (m.type == 0) {                                                    // Lambertian :20-25
+            RT_HCOUNT(HC_LAMBERT, 1);
             nd = h.n + unit;
             return true;
         }
+        RT_HCOUNT(HC_METAL, 1);
         nd = reflect(unit, h.n) + p * m.p;                                    // Metal :36-41 (roughness)
         return dot(nd, h.n) > (R)0;
     }
+    RT_HCOUNT(HC_DIELECTRIC, 1);
     R ratio = h.front ? ((R)1 / m.p) : m.p;                                   // Dielectric :51-83 (ior)
     R cos_t = js_min<R>(dot(unit * (R)-1, h.n), (R)1);
     R sin_t = sqrt((R)1 - cos_t * cos_t);
     bool reflect_it = ratio * sin_t > (R)1;
     if (!reflect_it) {                                                        // random drawn only if it can refract
+        RT_HCOUNT(HC_DIELECTRIC_SCHLICK, 1);
         R r0 = ((R)1 - ratio) / ((R)1 + ratio);
         r0 = r0 * r0;
         R refl = r0 + ((R)1 - r0) * pow5_rn((R)1 - cos_t);
@@ -166,6 +171,7 @@ RT_HD bool shade_segment(const SceneView<R>& sc, const Closest<R>& c, V3<R>& o, 
     const V3<R> unit = normalize(hit && m.type == 0 ? p : d);
     if (hit) {
         if (m.type == 3) {                                                    // Emissive (materials.js:87-96)
+            RT_HCOUNT(HC_EMISSIVE, 1);
             L = mk(T.x * m.c[0], T.y * m.c[1], T.z * m.c[2]);                 // emission
         } else {
             V3<R> nd, att;
@@ -177,6 +183,7 @@ RT_HD bool shade_segment(const SceneView<R>& sc, const Closest<R>& c, V3<R>& o, 
             }
         }
     } else {
+        RT_HCOUNT(HC_MISS, 1);
         const V3<R> bg = background(sc, d, unit);                             // world.background(ray)
         L = mk(T.x * bg.x, T.y * bg.y, T.z * bg.z);
     }

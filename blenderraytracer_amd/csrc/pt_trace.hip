@@ -109,8 +109,15 @@ __device__ __forceinline__ void add_totals(const Counters& c, const PixelResult&
 
 // The render's cancel word (Counters::cancel, mapped host memory written by rt_cancel / the progress
 // callback): read with system scope, so the read goes to host memory and not to a cached copy.
-__device__ __forceinline__ bool cancel_requested(const Counters& c) {
-    return c.cancel && __hip_atomic_load(const_cast<uint32_t*>(c.cancel), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+#ifndef RT_CANCEL_POLL
+#define RT_CANCEL_POLL 1          // A/B: 0 = the kernels never read the cancel word (the gates still run)
+#endif
+// copy: the wave's copy of the word (Counters::cancel); one line read by every wave measured 50 us per
+// read (RTOW 16 progressive batches: +4.5 % kernel time), the reads of one line being serialized
+__device__ __forceinline__ bool cancel_requested(const Counters& c, unsigned copy) {
+    return RT_CANCEL_POLL && c.cancel &&
+           __hip_atomic_load(const_cast<uint32_t*>(c.cancel) + (copy % kCancelCopies) * kCancelStride, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM) != 0;
 }
 // this batch leaves items untraced: its partials must not be reduced (one lane writes)
 __device__ __forceinline__ void mark_aborted(const Counters& c) {
@@ -230,7 +237,7 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
     acc[64 + lane] = 0;
     acc[128 + lane] = 0;
     __syncthreads();
-    if (args.c.cancel && __builtin_amdgcn_readfirstlane((int)cancel_requested(args.c))) {
+    if (args.c.cancel && __builtin_amdgcn_readfirstlane((int)cancel_requested(args.c, blockIdx.x))) {
         if (lane == 0) mark_aborted(args.c);  // the workgroup is one item: it is left untraced
         return;
     }
@@ -515,7 +522,7 @@ void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, c
         uint32_t it = 0;
         int stop = 0;
         if (lane == 0) {
-            stop = cancel_requested(args.c);
+            stop = cancel_requested(args.c, blockIdx.x * W + wave);
             it = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         it = (uint32_t)__builtin_amdgcn_readfirstlane((int)it);

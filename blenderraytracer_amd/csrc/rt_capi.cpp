@@ -155,11 +155,16 @@ inline int lookahead(int devices) { return kSlots * std::max(1, devices); }
 // The render's control words (rt_scene::ctl, mapped coherent host memory, read and written by the host
 // and by the kernels of every device): the cancel word, the sticky stop word and the samples the sums
 // hold (ReduceGate), and one `aborted` word per batch slot of the ring.
-constexpr int kCtlCancel = 0, kCtlStop = 1, kCtlDone = 2, kCtlAborted = 4;
-constexpr int kCtlWords = kCtlAborted + 64;
-static_assert(kCtlAborted + kSlots * RT_MAX_DEVICES + kSlots <= kCtlWords, "one aborted word per ring slot");
+// kCtlCancel: kCancelCopies copies of the cancel word, one per 128-B line (pt_launch.h).
+constexpr int kCtlStop = 1, kCtlDone = 2, kCtlAborted = 4;
+constexpr int kCtlCancel = 128;
+constexpr int kCtlWords = kCtlCancel + kCancelCopies * kCancelStride;
+static_assert(kCtlAborted + kSlots * RT_MAX_DEVICES + kSlots <= kCtlCancel, "one aborted word per ring slot");
 inline uint32_t ctl_load(const uint32_t* ctl, int k) { return __atomic_load_n(ctl + k, __ATOMIC_SEQ_CST); }
 inline void ctl_store(uint32_t* ctl, int k, uint32_t v) { __atomic_store_n(ctl + k, v, __ATOMIC_SEQ_CST); }
+inline void ctl_cancel(uint32_t* ctl, uint32_t v) {
+    for (int k = 0; k < kCancelCopies; ++k) ctl_store(ctl, kCtlCancel + k * kCancelStride, v);
+}
 
 // Everything one device holds for a scene: the scene arrays in its HBM, a stream, the running sums
 // and counters of the samples it traces, the pool's chunk partials and the work totals (scratch).
@@ -722,7 +727,7 @@ void rt_scene_destroy(rt_scene* sc) {
 int rt_cancel(rt_scene* sc) {
     if (!sc) return fail(RT_ERR_INVALID, "scene is NULL");
     sc->cancel.store(1);
-    if (sc->ctl) ctl_store(sc->ctl, kCtlCancel, 1);   // the queued batches stop at their next item
+    if (sc->ctl) ctl_cancel(sc->ctl, 1);   // the queued batches stop at their next item
     return RT_OK;
 }
 
@@ -800,7 +805,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     std::vector<DeviceState*> states;
     if ((rc = shard_states(sc, s, states))) return rc;
     sc->cancel.store(0);
-    ctl_store(sc->ctl, kCtlCancel, 0);
+    ctl_cancel(sc->ctl, 0);
     const size_t n = (size_t)cw * ch;
     const bool want_segs = out && out->segments, want_draws = out && out->draws;
     const bool pool = use_pool(s);
@@ -867,7 +872,8 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     // untraced items is never reduced (ReduceGate), nor is any batch after it, so the sums always hold
     // the batches [0, k) for some k.  For batches reduced on one stream in batch order: one device, or
     // the whole-batch split.  The split of every batch over devices observes a cancel between batches.
-    const bool gated = overlap && (nsh == 1 || whole);
+    static const bool item_cancel = !(getenv("RT_ITEM_CANCEL") && getenv("RT_ITEM_CANCEL")[0] == '0');   // A/B runs
+    const bool gated = item_cancel && overlap && (nsh == 1 || whole);
     if (gated) {
         HIP_TRY(hipSetDevice(h.device));
         HIP_TRY(h.gate_skip.ensure(1));
@@ -1036,13 +1042,13 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         const int be = sc->ckpt_done;
         if (merged && progress && be < s1 && progress((double)(be - s0) / (double)(s1 - s0), user)) {
             sc->cancel.store(1);
-            ctl_store(sc->ctl, kCtlCancel, 1);
+            ctl_cancel(sc->ctl, 1);
         }
         if (!merged || sc->cancel.load()) {
             if (gated) {
                 // the queued batches stop at their next item and are not reduced; once every stream has
                 // drained, the sums hold exactly the batches the gates committed
-                ctl_store(sc->ctl, kCtlCancel, 1);
+                ctl_cancel(sc->ctl, 1);
                 for (DeviceState* ds : states) ds->sync_all();
                 h.sync_all();
                 sc->ckpt_done = (int)ctl_load(sc->ctl, kCtlDone);

@@ -382,6 +382,11 @@ inline std::vector<int> peel_big_spheres(const HostScene& hs, std::vector<BuildP
 // cells per sphere of about cubic shape, every sphere registered in each cell its box padded by m
 // overlaps, in the cells' binary32 coordinates lo + k cs that the walk uses.  No grid when a sphere box
 // is not finite or the spheres are too few.
+// The two factors of the grid's exactness argument (pt_core.h closest_hit_grid, "grid_bound"): the
+// registration margin m = kGridMargin (B + E) and the origin bound grid_far = kGridFar (B + E).  A ray
+// point's error is at most 2^-19 (|o|_inf + B) <= 2^-19 (kGridFar + 1) (B + E), which must not exceed m.
+constexpr double kGridMargin = 0x1p-12, kGridFar = 0x1p6;
+static_assert(0x1p-19 * (kGridFar + 1) <= kGridMargin, "grid_far too large for the registration margin");
 inline void build_grid(HostScene& hs, const std::vector<BuildPrim>& prims) {
     hs.grid_cell.clear();
     hs.grid_ids.clear();
@@ -400,7 +405,7 @@ inline void build_grid(HostScene& hs, const std::vector<BuildPrim>& prims) {
         E = std::max(E, hi[a] - lo[a]);
     }
     if (!(B + E > 0) || !(B + E < 1e30)) return;
-    const double m = 0x1p-12 * (B + E);
+    const double m = kGridMargin * (B + E);
     double ext[3], vol = 1;
     for (int a = 0; a < 3; ++a) {
         lo[a] -= m;
@@ -425,7 +430,7 @@ inline void build_grid(HostScene& hs, const std::vector<BuildPrim>& prims) {
         if ((double)fhi < hi[a]) fhi = std::nextafter(fhi, INFINITY);
         hs.grid_hi[a] = fhi;
     }
-    hs.grid_far = (float)(0x1p6 * (B + E));
+    hs.grid_far = (float)(kGridFar * (B + E));
     if (total > (1LL << 22)) { hs.grid_n[0] = hs.grid_n[1] = hs.grid_n[2] = 0; return; }
     auto range = [&](const BuildPrim& p, int a, int& k0, int& k1) {
         const double c = (double)hs.grid_cs[a], o = (double)hs.grid_lo[a];

@@ -137,10 +137,11 @@ class GpuRayTracer:
         """RayTracer.render: fills image_data (RGBA8) and float_data (post-gamma RGBA float).
         Returns a dict of the requested host arrays (mean, post, rgba8, segments, draws, preview).
         resume: a checkpoint() result to continue from (rt_render_resume).
-        devices: HIP ordinals to split every sample batch over (multi-GPU; may repeat a device).
-        "preview" in want (with batch_samples): image_data shows the frame of the samples done so far
-        when on_progress runs (rt_output.preview_rgba8); a cancel (on_progress returning True) then
-        leaves that frame of the checkpointed samples in image_data and raises RuntimeError(RT_ERR_CANCELLED)."""
+        devices: HIP ordinals to deal the sample batches to (multi-GPU; may repeat a device).
+        "preview" in want (with batch_samples): when on_progress runs, image_data (full frame) and the
+        returned "preview" array hold the frame of the samples done so far (rt_output.preview_rgba8); a
+        cancel (on_progress returning True, or rt_cancel) leaves the frame of the checkpointed samples
+        there and raises RuntimeError(RT_ERR_CANCELLED)."""
         lib = capi.load_library()
         scene = self.scene_handle()
         st = self.settings(crop=crop, batch_samples=batch_samples, devices=devices)
@@ -165,6 +166,8 @@ class GpuRayTracer:
         if "preview" in want:
             res["preview"] = np.zeros((ch, cw, 4), dtype=np.uint8)
             out.preview_rgba8 = res["preview"].ctypes.data_as(C.POINTER(C.c_uint8))
+            if crop is None:                 # the running frame, as the reference's canvas between rows
+                self.image_data = res["preview"]
         stats = capi.Stats()
         cb = capi.PROGRESS_FN(lambda f, u: int(bool(on_progress(f)) if on_progress else 0))
         if resume is None:

@@ -1,0 +1,25 @@
+"""Progressive-render cost probe (DEV TOOL): config 3 as one batch and as 16 batches of 32 spp, each
+rendered `reps` times; prints the median kernel and wall time.
+usage: python scripts/probe_progressive.py [reps]"""
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: F401,E402
+import bench  # noqa: E402
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+cfg = bench.CONFIGS["rtow"]
+rt = bench.make_tracer(cfg, "f64", 1, 0)
+rt.render()
+for b in (0, 32, 0, 32):
+    ks, ws = [], []
+    for _ in range(reps):
+        t = time.perf_counter()
+        rt.render(batch_samples=b)
+        ws.append(time.perf_counter() - t)
+        ks.append(rt.last_stats.kernel_ms)
+    print(f"batch {b}: kernel median {statistics.median(ks):.1f} ms (min {min(ks):.1f}), wall median "
+          f"{statistics.median(ws) * 1e3:.1f} ms", flush=True)

@@ -291,8 +291,9 @@ extern "C" int ptc_bvh_info(const rt_scene_desc* d, int* depth, int* nodes2, int
     return 0;
 }
 
-// Work totals of the two-child walk (s->accel != 4) or the grid walk (4) over a crop (host experiments
-// on BVH quality, TEST/DEV TOOL): out = {segments, nodes or cells, sphere tests, triangle tests}
+// Work totals of the two-child walk (s->accel other than below), the grid walk (4) or World order
+// (RT_ACCEL_BRUTE) over a crop (host experiments on BVH quality and the instruction-floor model,
+// TEST/DEV TOOL): out = {segments, nodes or cells, sphere tests, triangle tests}
 extern "C" int ptc_work(const rt_scene_desc* d, const rt_settings* s, double* out) {
     HostView<double> hv;
     if (!hv.init(d)) return -1;
@@ -314,11 +315,23 @@ extern "C" int ptc_work(const rt_scene_desc* d, const rt_settings* s, double* ou
         for (int cx = 0; cx < im.cw; ++cx) {
             double acc[3] = {0, 0, 0};
             const PixelResult r = s->accel == 4 ? trace_pixel<double, true, ACC_GRID>(hv.v, im, cx, cy, im.s_end, acc)
+                                : s->accel == RT_ACCEL_BRUTE ? trace_pixel<double, true, ACC_BRUTE>(hv.v, im, cx, cy, im.s_end, acc)
                                                 : trace_pixel<double, true, ACC_BVH_STACK>(hv.v, im, cx, cy, im.s_end, acc, stk);
             out[0] += r.segments; out[1] += r.work.nodes; out[2] += r.work.spheres; out[3] += r.work.tris;
         }
     return 0;
 }
+
+#ifdef RT_HOST_COUNTERS
+// event counts of the kernel's code on the host (pt_core.h RT_HCOUNT, the instruction-floor model, DEV TOOL)
+namespace rt { unsigned long long rt_host_count[16]; }
+extern "C" void ptc_host_counts(unsigned long long* out, int reset) {
+    for (int k = 0; k < 16; ++k) {
+        out[k] = rt::rt_host_count[k];
+        if (reset) rt::rt_host_count[k] = 0;
+    }
+}
+#endif
 
 // pow5_rn (pt_path.h) on the host, for the comparison with libm pow (TEST TOOL)
 extern "C" void ptc_pow5(const double* x, double* out, long long n) {

@@ -87,6 +87,31 @@ def bvh_rays(packed, n, seed, host_n=None):
     return rays[:m], t[:m], kind[:m], idx[:m]
 
 
+EVENTS = ["f64_sphere_tests", "disc_nonneg", "second_root", "accept", "lambertian", "metal", "dielectric", "emissive",
+          "miss", "samples", "sphere_draw_rounds", "disk_draw_rounds", "filter_tests", "dielectric_schlick"]
+
+
+def event_counts(packed, settings_list, walk):
+    """Events per segment of the kernel's own code run on the CPU over the given crops (pt_core.h
+    RT_HCOUNT; the instruction-floor model of bench.py): walk "grid" | "bvh" | "brute" as the GPU runs it."""
+    L = lib(("RT_HOST_COUNTERS=1",))
+    L.ptc_work.argtypes = [C.POINTER(capi.SceneDesc), C.POINTER(capi.Settings), C.POINTER(C.c_double)]
+    L.ptc_host_counts.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    cnt = (C.c_ulonglong * 16)()
+    L.ptc_host_counts(cnt, 1)
+    out = (C.c_double * 4)()
+    tot = [0.0] * 4
+    for st in settings_list:
+        st.accel = {"grid": 4, "bvh": capi.RT_ACCEL_BVH, "brute": capi.RT_ACCEL_BRUTE}[walk]
+        assert L.ptc_work(C.byref(packed.desc), C.byref(st), out) == 0
+        tot = [a + b for a, b in zip(tot, out)]
+    L.ptc_host_counts(cnt, 1)
+    seg = max(tot[0], 1.0)
+    res = {"segments": tot[0], "walk_steps": tot[1] / seg, "sphere_tests_work": tot[2] / seg, "tri_tests": tot[3] / seg}
+    res.update({n: cnt[k] / seg for k, n in enumerate(EVENTS)})
+    return res
+
+
 def render(packed, settings, L=None):
     """Per-pixel linear means, segment and draw counts computed by the kernel's own code on the CPU
     (`L`: a variant library from lib(defines))."""
