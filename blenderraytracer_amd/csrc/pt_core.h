@@ -142,6 +142,7 @@ struct SceneView {
     const int* box_mat;
     const int* tri_mat;            // per triangle (mesh triangles carry the mesh's material)
     const MatRec<R>* mats;
+    int num_mats;
     const int* perm;               // World.cloudNoise.p[512]
     // acceleration structure (closest_hit_bvh): planes and boxes are tested brute force with their
     // World.objects index, spheres and triangles through one BVH each over leaf-order copies

@@ -154,7 +154,7 @@ struct PixelResult { uint32_t segments, draws; Work work; uint64_t cyc[3]; };
 // then in `L`, otherwise (o, d, T, depth) describe the next segment.
 template <class R>
 RT_HD bool shade_segment(const SceneView<R>& sc, const Closest<R>& c, V3<R>& o, V3<R>& d, V3<R>& T, int& depth,
-                         Rng<R>& g, V3<R>& L) {
+                         Rng<R>& g, V3<R>& L, const MatRec<R>* mats = nullptr) {
     bool done = true;
     L = mk<R>(0, 0, 0);
     const bool hit = c.kind != HIT_NONE;
@@ -163,7 +163,7 @@ RT_HD bool shade_segment(const SceneView<R>& sc, const Closest<R>& c, V3<R>& o, 
     V3<R> p = mk<R>(0, 0, 0);
     if (hit) {
         h = hit_record(sc, o, d, c);
-        m = sc.mats[h.mat];
+        m = mats ? mats[h.mat] : sc.mats[h.mat];            // mats: an LDS copy (RT_MAT_LDS A/B)
         if (m.type <= 1) p = random_in_unit_sphere(g);                       // Lambertian / Metal's only draws
     }
     // one normalize for every lane (see scatter): Lambertian's p, else the ray direction (Metal,

@@ -203,7 +203,18 @@ constexpr int kParkDoubles = 3, kParkInts = 6;
 template <class R, int ACC>
 constexpr bool parks() { return RT_PARK != 0 && sizeof(R) == 8 && uses_stack<ACC>(); }
 
-template <class R, bool COUNT, int ACC>
+// RT_DEFER_REGEN = K: a lane whose sample finished waits, without tracing, until K lanes of its wave wait
+// (or none traces), and the waiting lanes then start their next samples together: the sample set-up
+// (keys, the lens disk's rejection loop, the binary64 camera ray) runs for many lanes at once instead
+// of for the few that finish in each iteration (RTOW +4.8 %).  A wave's execution still
+// depends only on its items, so the sums stay bit-reproducible; K = 1 is the undeferred loop.
+#ifndef RT_DEFER_REGEN
+#define RT_DEFER_REGEN 16
+#endif
+
+// CANCEL: the launch carries a cancel word (progressive renders, Counters::cancel); the instantiation
+// without it holds no polling code (the poll's code alone cost 1.4 % on RTOW)
+template <class R, bool COUNT, int ACC, bool CANCEL>
 __global__ __launch_bounds__(64, (waves_per_simd<R, ACC>()))
 void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const int tiles, const int chunk) {
     const ImageParams& im = args.im;
@@ -237,9 +248,11 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
     acc[64 + lane] = 0;
     acc[128 + lane] = 0;
     __syncthreads();
-    if (args.c.cancel && __builtin_amdgcn_readfirstlane((int)cancel_requested(args.c, blockIdx.x))) {
-        if (lane == 0) mark_aborted(args.c);  // the workgroup is one item: it is left untraced
-        return;
+    if constexpr (CANCEL) {
+        if (__builtin_amdgcn_readfirstlane((int)cancel_requested(args.c, blockIdx.x))) {
+            if (lane == 0) mark_aborted(args.c);  // the workgroup is one item: it is left untraced
+            return;
+        }
     }
     const int ci = blockIdx.x / tiles, tile = blockIdx.x % tiles;
     const Tile tl = tile_of(im, tile);
@@ -272,49 +285,53 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
     uint32_t next = 64;                       // items [0, 64) are dealt to lanes 0..63 up front
     bool live = (uint32_t)lane < total;
     if (live) begin_item((uint32_t)lane);
+    bool waiting = false;                     // the lane's sample is done, its next not yet started
     while (live) {                            // lanes only ever leave this loop, so every live lane
         const uint64_t t0 = RT_TICK();        // has seen every update of `next`
-        if constexpr (PARK) {
-            park_d[0] = (double)T.x; park_d[64] = (double)T.y; park_d[128] = (double)T.z;
-            park_i[0] = (uint32_t)depth; park_i[64] = isegs; park_i[128] = m;
-            park_i[192] = g.key; park_i[256] = g.k; park_i[320] = res.segments;
-        }
-        const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, res.work, stk);
-        if constexpr (PARK) {
-            // the walk's stack stores may alias these slots as far as the compiler can tell: the
-            // values are reloaded, not forwarded, so their registers are free during the walk
-            T = mk<R>((R)park_d[0], (R)park_d[64], (R)park_d[128]);
-            depth = (int)park_i[0]; isegs = park_i[64]; m = park_i[128];
-            g.key = park_i[192]; g.k = park_i[256]; res.segments = park_i[320];
-            if (COUNT) q = (size_t)(tl.y0 + (int)(m / (uint32_t)vw)) * im.cw + (tl.x0 + (int)(m % (uint32_t)vw));
-        }
-        const uint64_t t1 = RT_TICK();
-        if (RT_PROFILE) res.cyc[0] += t1 - t0;
-        ++res.segments;
-        ++isegs;
-        V3<R> L;
-        const bool done = shade_segment(sc, c, o, d, T, depth, g, L);
-        const uint64_t t2 = RT_TICK();
-        if (RT_PROFILE) res.cyc[1] += t2 - t1;
-        const uint64_t need = __ballot(done);
-        if (need) {
-            if (COUNT && done) {
-                if (args.c.segs) atomicAdd(args.c.segs + q, isegs);
-                if (args.c.draws) atomicAdd(args.c.draws + q, g.k);
+        if (!waiting) {
+            if constexpr (PARK) {
+                park_d[0] = (double)T.x; park_d[64] = (double)T.y; park_d[128] = (double)T.z;
+                park_i[0] = (uint32_t)depth; park_i[64] = isegs; park_i[128] = m;
+                park_i[192] = g.key; park_i[256] = g.k; park_i[320] = res.segments;
             }
-            // add the finished samples' radiance to its pixel's partial: non-returning LDS atomics
-            // (ds_add_f64), no wait.  Lanes that finish samples of the same pixel in one iteration
-            // are combined by the LDS atomic unit in its fixed lane order.
-            if (done) {
+            const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, res.work, stk);
+            if constexpr (PARK) {
+                // the walk's stack stores may alias these slots as far as the compiler can tell: the
+                // values are reloaded, not forwarded, so their registers are free during the walk
+                T = mk<R>((R)park_d[0], (R)park_d[64], (R)park_d[128]);
+                depth = (int)park_i[0]; isegs = park_i[64]; m = park_i[128];
+                g.key = park_i[192]; g.k = park_i[256]; res.segments = park_i[320];
+                if (COUNT) q = (size_t)(tl.y0 + (int)(m / (uint32_t)vw)) * im.cw + (tl.x0 + (int)(m % (uint32_t)vw));
+            }
+            const uint64_t t1 = RT_TICK();
+            if (RT_PROFILE) res.cyc[0] += t1 - t0;
+            ++res.segments;
+            ++isegs;
+            V3<R> L;
+            waiting = shade_segment(sc, c, o, d, T, depth, g, L);
+            if (RT_PROFILE) res.cyc[1] += RT_TICK() - t1;
+            if (waiting) {
+                if (COUNT) {
+                    if (args.c.segs) atomicAdd(args.c.segs + q, isegs);
+                    if (args.c.draws) atomicAdd(args.c.draws + q, g.k);
+                }
+                // add the finished sample's radiance to its pixel's partial: non-returning LDS atomics
+                // (ds_add_f64), no wait.  Lanes that finish samples of the same pixel in one iteration
+                // are combined by the LDS atomic unit in its fixed lane order.
                 __hip_atomic_fetch_add(&acc[m], (double)L.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 __hip_atomic_fetch_add(&acc[64 + m], (double)L.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 __hip_atomic_fetch_add(&acc[128 + m], (double)L.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            if (done) {
+        }
+        const uint64_t t2 = RT_TICK();
+        const uint64_t need = __ballot(waiting);
+        if (need && (__popcll(need) >= RT_DEFER_REGEN || __ballot(!waiting) == 0)) {
+            if (waiting) {
                 const uint32_t k = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0));
                 live = k < total;
                 if (live) begin_item(k);
+                waiting = false;
             }
             next += (uint32_t)__popcll(need);
         }
@@ -345,7 +362,7 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
 template <class R, bool COUNT, int ACC>
 __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __restrict__ part, const int tiles,
                                           const int chunk, const unsigned item, double* acc, BvhStack stk,
-                                          PixelResult& res, const int lane) {
+                                          PixelResult& res, const int lane, const MatRec<R>* lmats = nullptr) {
     const ImageParams& im = args.im;
     const SceneView<R>& sc = args.sc;
     const int ci = item / tiles, tile = item % tiles;     // (unsigned, as blockIdx.x)
@@ -378,36 +395,37 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
     uint32_t next = 64;                       // items [0, 64) are dealt to lanes 0..63 up front
     bool live = (uint32_t)lane < total;
     if (live) begin_item((uint32_t)lane);
+    bool waiting = false;                     // as trace_pool_kernel (RT_DEFER_REGEN)
     while (live) {                            // lanes only ever leave this loop, so every live lane
         const uint64_t t0 = RT_TICK();        // has seen every update of `next`
-        const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, res.work, stk);
-        const uint64_t t1 = RT_TICK();
-        if (RT_PROFILE) res.cyc[0] += t1 - t0;
-        ++res.segments;
-        ++isegs;
-        V3<R> L;
-        const bool done = shade_segment(sc, c, o, d, T, depth, g, L);
-        const uint64_t t2 = RT_TICK();
-        if (RT_PROFILE) res.cyc[1] += t2 - t1;
-        const uint64_t need = __ballot(done);
-        if (need) {
-            if (COUNT && done) {
-                if (args.c.segs) atomicAdd(args.c.segs + q, isegs);
-                if (args.c.draws) atomicAdd(args.c.draws + q, g.k);
-            }
-            // add the finished samples' radiance to its pixel's partial: non-returning LDS atomics
-            // (ds_add_f64), no wait.  Lanes that finish samples of the same pixel in one iteration
-            // are combined by the LDS atomic unit in its fixed lane order.
-            if (done) {
+        if (!waiting) {
+            const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, res.work, stk);
+            const uint64_t t1 = RT_TICK();
+            if (RT_PROFILE) res.cyc[0] += t1 - t0;
+            ++res.segments;
+            ++isegs;
+            V3<R> L;
+            waiting = shade_segment(sc, c, o, d, T, depth, g, L, lmats);
+            if (RT_PROFILE) res.cyc[1] += RT_TICK() - t1;
+            if (waiting) {
+                if (COUNT) {
+                    if (args.c.segs) atomicAdd(args.c.segs + q, isegs);
+                    if (args.c.draws) atomicAdd(args.c.draws + q, g.k);
+                }
                 __hip_atomic_fetch_add(&acc[m], (double)L.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 __hip_atomic_fetch_add(&acc[64 + m], (double)L.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 __hip_atomic_fetch_add(&acc[128 + m], (double)L.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            if (done) {
+        }
+        const uint64_t t2 = RT_TICK();
+        const uint64_t need = __ballot(waiting);
+        if (need && (__popcll(need) >= RT_DEFER_REGEN || __ballot(!waiting) == 0)) {
+            if (waiting) {
                 const uint32_t k = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0));
                 live = k < total;
                 if (live) begin_item(k);
+                waiting = false;
             }
             next += (uint32_t)__popcll(need);
         }
@@ -485,7 +503,7 @@ __device__ __forceinline__ void copy_nodes_lds(const SceneView<R>& sc, rt_u4* bo
 // ACC_GRID_LDS: the same workgroups and queue with the uniform grid's cell offsets and records
 // (binary64: the 16-B binary32 filters; binary32: the whole 32-B records) in LDS instead of nodes: the
 // filter rejections, most of a grid walk's record tests, no longer touch the vector memory path.
-template <class R, bool COUNT, int ACC>
+template <class R, bool COUNT, int ACC, bool CANCEL>
 __global__ __launch_bounds__((64 * lds_waves<R, ACC>()), (waves_per_simd<R, ACC>()))
 void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, const int tiles, const int chunk,
                            const int items, const int qi) {
@@ -495,7 +513,9 @@ void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, c
     // for the grid [records][cell offsets]
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_dyn[];
     __shared__ double acc_all[W * 3 * 64];
+    __shared__ uint32_t stop_flag;            // CANCEL: wave 0 polls the cancel word, the others read this
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (CANCEL && threadIdx.x == 0) stop_flag = 0;
     BvhStack stk{nullptr, 0};
     if constexpr (ACC == ACC_GRID_LDS) {
         rt_u4* grec = reinterpret_cast<rt_u4*>(lds_dyn);
@@ -515,6 +535,14 @@ void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, c
     acc[lane] = 0;
     acc[64 + lane] = 0;
     acc[128 + lane] = 0;
+    const MatRec<R>* lmats = nullptr;
+#if RT_MAT_LDS
+    if constexpr (ACC == ACC_GRID_LDS) {      // A/B: the material records after the grid's copy
+        MatRec<R>* mm = reinterpret_cast<MatRec<R>*>(lds_dyn + ((grid_lds_bytes(sc) + 15) & ~(size_t)15));
+        for (int k = threadIdx.x; k < sc.num_mats; k += 64 * W) mm[k] = sc.mats[k];
+        lmats = mm;
+    }
+#endif
     __syncthreads();
     uint32_t* queue = g_pool_queue + 2 * qi;
     PixelResult res{0, 0, {0, 0, 0}, {0, 0, 0}};
@@ -522,16 +550,20 @@ void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, c
         uint32_t it = 0;
         int stop = 0;
         if (lane == 0) {
-            stop = cancel_requested(args.c, blockIdx.x * W + wave);
+            if constexpr (CANCEL) {
+                if (wave == 0 && cancel_requested(args.c, blockIdx.x))
+                    __hip_atomic_store(&stop_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                stop = (int)__hip_atomic_load(&stop_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
             it = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         it = (uint32_t)__builtin_amdgcn_readfirstlane((int)it);
         if (it >= (uint32_t)items) break;
-        if (__builtin_amdgcn_readfirstlane(stop)) {   // a cancel: this item (and the rest) stay untraced
+        if (CANCEL && __builtin_amdgcn_readfirstlane(stop)) {   // a cancel: this item (and the rest) stay untraced
             if (lane == 0) mark_aborted(args.c);
             break;
         }
-        pool_item<R, COUNT, ACC>(args, part, tiles, chunk, it, acc, stk, res, lane);
+        pool_item<R, COUNT, ACC>(args, part, tiles, chunk, it, acc, stk, res, lane, lmats);
     }
     add_totals<ACC>(args.c, res, lane);
     if (lane == 0) {
@@ -643,6 +675,11 @@ size_t pool_partial_bytes(int cw, int ch, int ns, bool tri_bvh, int chunk_overri
 #ifndef RT_LDS_GRID
 #define RT_LDS_GRID 1
 #endif
+// RT_MAT_LDS (A/B): the grid LDS kernel also stages the material records in LDS (the budget check then
+// counts them: fewer workgroups per CU when they do not fit beside the grid)
+#ifndef RT_MAT_LDS
+#define RT_MAT_LDS 0
+#endif
 template <class R>
 static size_t lds_grid_bytes(const SceneView<R>& sc) {
     static int v = -1;
@@ -652,8 +689,9 @@ static size_t lds_grid_bytes(const SceneView<R>& sc) {
     }
     if (v < 1 || sc.num_grid_cells <= 0) return 0;
     constexpr int W = lds_waves<R, ACC_GRID_LDS>();
-    const size_t b = (grid_lds_bytes(sc) + 15) & ~(size_t)15;
-    const size_t budget = 160 * 1024 / (4 * waves_per_simd<R, ACC_GRID_LDS>() / W);
+    const size_t b = ((grid_lds_bytes(sc) + 15) & ~(size_t)15) + (RT_MAT_LDS ? sizeof(MatRec<R>) * (size_t)sc.num_mats : 0);
+    // RT_MAT_LDS: one workgroup per CU fewer (4 instead of 5 binary64 grid workgroups)
+    const size_t budget = 160 * 1024 / (4 * waves_per_simd<R, ACC_GRID_LDS>() / W - (RT_MAT_LDS ? 1 : 0));
     return b + (size_t)W * 3 * 64 * 8 + 256 <= budget ? b : 0;
 }
 
@@ -697,14 +735,22 @@ static void launch_pool_kernel(const TraceArgs<R>& a, bool count, double* part, 
             constexpr int W = lds_waves<R, LACC>();
             const int resident = device_cus() * 4 * waves_per_simd<R, LACC>() / W;
             const int grid = (int)std::min<long long>(resident, (items + W - 1) / W);
-            if (count) hipLaunchKernelGGL((trace_pool_lds_kernel<R, true, LACC>), dim3(grid), dim3(64 * W), lb, stream, a, part, tiles, chunk, (int)items, qi);
-            else hipLaunchKernelGGL((trace_pool_lds_kernel<R, false, LACC>), dim3(grid), dim3(64 * W), lb, stream, a, part, tiles, chunk, (int)items, qi);
+#define RT_LDS_LAUNCH(C, X) hipLaunchKernelGGL((trace_pool_lds_kernel<R, C, LACC, X>), dim3(grid), dim3(64 * W), lb, stream, \
+                                            a, part, tiles, chunk, (int)items, qi)
+            if (a.c.cancel) { if (count) RT_LDS_LAUNCH(true, true); else RT_LDS_LAUNCH(false, true); }
+            else if (count) RT_LDS_LAUNCH(true, false);
+            else RT_LDS_LAUNCH(false, false);
+#undef RT_LDS_LAUNCH
             return;
         }
     }
     const size_t lds = pool_lds_bytes<ACC>(a.sc);
-    if (count) hipLaunchKernelGGL((trace_pool_kernel<R, true, ACC>), dim3(tiles * chunks), dim3(64), lds, stream, a, part, tiles, chunk);
-    else hipLaunchKernelGGL((trace_pool_kernel<R, false, ACC>), dim3(tiles * chunks), dim3(64), lds, stream, a, part, tiles, chunk);
+#define RT_POOL_LAUNCH(C, X) hipLaunchKernelGGL((trace_pool_kernel<R, C, ACC, X>), dim3(tiles * chunks), dim3(64), lds, stream, \
+                                             a, part, tiles, chunk)
+    if (a.c.cancel) { if (count) RT_POOL_LAUNCH(true, true); else RT_POOL_LAUNCH(false, true); }
+    else if (count) RT_POOL_LAUNCH(true, false);
+    else RT_POOL_LAUNCH(false, false);
+#undef RT_POOL_LAUNCH
 }
 
 template <class R, int ACC>

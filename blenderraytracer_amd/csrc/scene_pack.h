@@ -603,6 +603,7 @@ void fill_view_constants(SceneView<R>& v, const HostScene& hs, const rt_scene_de
     v.num_spheres = (int)hs.sphere_r.size();
     v.num_prims = hs.num_prims;
     v.num_planes = (int)hs.plane_mat.size();
+    v.num_mats = d.num_materials;
     v.num_boxes = (int)hs.box_mat.size();
     v.num_sphere_nodes = (int)hs.sphere_bvh.size();
     v.num_tri_nodes = (int)hs.tri_bvh.size();
