@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -327,6 +328,26 @@ inline std::vector<Bvh2Node> make_wide(const std::vector<BvhNode>& t) {
     for (size_t i = 0; i < t.size(); ++i)           // preorder: a subtree's nodes stay close in memory
         if (t[i].fc == 0) map[i] = k++;
     out.resize(k);
+    // RT_BVH_LAYOUT=top (A/B, mesh scenes): the top levels' inner nodes first, breadth first (the first
+    // 2048: the nodes every walk reads, packed on 64 KB of lines), then each remaining subtree in
+    // preorder, instead of one preorder array
+    static const bool top_first = getenv("RT_BVH_LAYOUT") && !strcmp(getenv("RT_BVH_LAYOUT"), "top");
+    if (top_first && k > 2048) {
+        std::vector<int> order;                     // tree indices of the inner nodes, new order
+        std::vector<char> taken(t.size(), 0);
+        std::vector<int> q{0};
+        for (size_t h = 0; h < q.size() && order.size() < 2048; ++h) {
+            const int i = q[h];
+            order.push_back(i);
+            taken[i] = 1;
+            const int l = i + 1, r = t[l].skip;
+            for (int c : {l, r})
+                if (t[c].fc == 0) q.push_back(c);
+        }
+        for (size_t i = 0; i < t.size(); ++i)
+            if (t[i].fc == 0 && !taken[i]) order.push_back((int)i);   // preorder of the rest
+        for (size_t n = 0; n < order.size(); ++n) map[order[n]] = (int)n;
+    }
     auto ref = [&](int i) { return t[i].fc ? ~t[i].fc : map[i]; };
     for (size_t i = 0; i < t.size(); ++i) {
         if (t[i].fc != 0) continue;

@@ -152,7 +152,9 @@ def test_cancel_via_progress(gpu):
     rt = _rtow(64, 36, 16)
     with pytest.raises(RuntimeError, match="CANCELLED"):
         rt.render(batch_samples=1, on_progress=lambda f: True)
-    assert rt.checkpoint()[1] == 4            # the first batch and the three queued behind it
+    # the first batch, plus those of the three queued behind it that were reduced before the cancel
+    # word reached them (they stop at their next item and are not reduced: the checkpoint is a prefix)
+    assert 1 <= rt.checkpoint()[1] <= 4
 
 
 def test_max_depth_zero_is_black(gpu):
@@ -246,7 +248,8 @@ def test_checkpoint_resume_is_bit_exact(gpu):
     with pytest.raises(RuntimeError, match="CANCELLED"):
         rt.render(batch_samples=1, on_progress=lambda f: calls.append(f) or len(calls) >= 2)
     sums, done = rt.checkpoint()
-    assert done == 5 and sums.shape == (54, 96, 3)     # cancelled after batch 2: batches 3 to 5 were in flight
+    # cancelled after batch 2: of batches 3 to 5 (queued) those reduced before the cancel reached them
+    assert 2 <= done <= 5 and sums.shape == (54, 96, 3)
     rt.close()
     rt2 = _rtow(96, 54, 10)
     res = rt2.render(want=("mean",), resume=(sums, done), batch_samples=1)
