@@ -517,12 +517,18 @@ napi_value checkpoint(napi_env env, napi_callback_info info) {
     SceneBox* box = argc ? get_box(env, argv[0]) : nullptr;
     if (!box || !box->sc) return throw_err(env, "checkpoint(scene)");
     if (box->busy) return throw_err(env, "checkpoint: a render is in flight");
-    std::vector<double> sums(box->last_pixels * 3);
+    // the sums go straight from the device into the ArrayBuffer handed to JS (no staging vector: a
+    // cancelled config-3 render's 50 MB checkpoint is part of the cancel's return time)
+    const size_t count = box->last_pixels * 3;
+    napi_value ab, arr;
+    void* p = nullptr;
+    NAPI_OK(napi_create_arraybuffer(env, count * sizeof(double), &p, &ab));
     int32_t done = 0;
-    if (rt_render_checkpoint(box->sc, sums.data(), sums.size(), &done) != RT_OK) return throw_err(env, rt_last_error());
+    if (rt_render_checkpoint(box->sc, static_cast<double*>(p), count, &done) != RT_OK) return throw_err(env, rt_last_error());
+    NAPI_OK(napi_create_typedarray(env, napi_float64_array, count, ab, 0, &arr));
     napi_value res, d;
     NAPI_OK(napi_create_object(env, &res));
-    NAPI_OK(napi_set_named_property(env, res, "sums", to_typed(env, sums, napi_float64_array)));
+    NAPI_OK(napi_set_named_property(env, res, "sums", arr));
     NAPI_OK(napi_create_int32(env, done, &d));
     NAPI_OK(napi_set_named_property(env, res, "samplesDone", d));
     return res;
