@@ -14,3 +14,5 @@ echo "-- grid from global memory (RT_LDS_GRID=0): survivor masks there too (gcom
 RT_LDS_GRID=0 timeout -k 10 120 bash scripts/ab_lib.sh "rtow 128 f64" cur gcomp >> $L 2>&1 || exit 1
 echo "-- RT_PROFILE split (RTOW 256 spp f64)" >> $L
 RT_HIP_LIB=blenderraytracer_amd/lib/variants/prof.so timeout -k 10 100 python scripts/probe_speed.py rtow 256 f64 >> $L 2>&1 || exit 1
+echo "-- filter loop unroll (cur = compiler's choice)" >> $L
+timeout -k 10 200 bash scripts/ab_lib.sh "rtow 256 f64" cur fu2 fu4 >> $L 2>&1 || exit 1
