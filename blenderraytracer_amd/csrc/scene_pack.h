@@ -328,26 +328,6 @@ inline std::vector<Bvh2Node> make_wide(const std::vector<BvhNode>& t) {
     for (size_t i = 0; i < t.size(); ++i)           // preorder: a subtree's nodes stay close in memory
         if (t[i].fc == 0) map[i] = k++;
     out.resize(k);
-    // RT_BVH_LAYOUT=top (A/B, mesh scenes): the top levels' inner nodes first, breadth first (the first
-    // 2048: the nodes every walk reads, packed on 64 KB of lines), then each remaining subtree in
-    // preorder, instead of one preorder array
-    static const bool top_first = getenv("RT_BVH_LAYOUT") && !strcmp(getenv("RT_BVH_LAYOUT"), "top");
-    if (top_first && k > 2048) {
-        std::vector<int> order;                     // tree indices of the inner nodes, new order
-        std::vector<char> taken(t.size(), 0);
-        std::vector<int> q{0};
-        for (size_t h = 0; h < q.size() && order.size() < 2048; ++h) {
-            const int i = q[h];
-            order.push_back(i);
-            taken[i] = 1;
-            const int l = i + 1, r = t[l].skip;
-            for (int c : {l, r})
-                if (t[c].fc == 0) q.push_back(c);
-        }
-        for (size_t i = 0; i < t.size(); ++i)
-            if (t[i].fc == 0 && !taken[i]) order.push_back((int)i);   // preorder of the rest
-        for (size_t n = 0; n < order.size(); ++n) map[order[n]] = (int)n;
-    }
     auto ref = [&](int i) { return t[i].fc ? ~t[i].fc : map[i]; };
     for (size_t i = 0; i < t.size(); ++i) {
         if (t[i].fc != 0) continue;
@@ -395,9 +375,10 @@ inline std::vector<int> peel_big_spheres(const HostScene& hs, std::vector<BuildP
 }
 
 #ifndef RT_GRID_LAMBDA
-#define RT_GRID_LAMBDA 0.25       // cells per sphere (before rounding each axis up): RTOW 256 spp f64 / f32
-#endif                            // 0.0625 8667 / 11281, 0.125 8765 / 11497, 0.25 8817 / 11625, 0.35 8750 /
-                                  // 11577, 0.5 8718 / 11515, 1 8574 / 11346, 2 8135 / 10930, 4 7854 / 10515
+#define RT_GRID_LAMBDA 0.09       // cells per sphere (before rounding each axis up).  RTOW 256 spp f64 / f32,
+#endif                            // round 4 (survivor masks, deferred regeneration): 0.0625 10154 / -,
+                                  // 0.09 10157 / 13052, 0.125 10073 / 12871, 0.25 9911 / 13183, 0.35 9771 / -
+                                  // (round 3, before the masks: 0.25 best, 0.0625 -1.7 %)
 // Uniform grid over the spheres of the sphere tree (closest_hit_grid, pt_core.h): the box of those
 // spheres padded by m = 2^-12 (B + E) (B: largest |coordinate|, E: largest extent), ~RT_GRID_LAMBDA
 // cells per sphere of about cubic shape, every sphere registered in each cell its box padded by m

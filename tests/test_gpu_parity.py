@@ -157,6 +157,22 @@ def test_cancel_via_progress(gpu):
     assert 1 <= rt.checkpoint()[1] <= 4
 
 
+def test_cancel_between_batches_in_sample_order(gpu):
+    """Without the pool's overlapped batches (sample order) a cancel is observed between batches: the
+    batches already queued complete (the first and the three behind it), and the checkpoint resumes
+    bit-exactly."""
+    rt = _rtow(64, 36, 16)
+    rt.sum_order = capi.RT_SUM_SAMPLE_ORDER
+    full = rt.render(want=("mean",), batch_samples=1)
+    with pytest.raises(RuntimeError, match="CANCELLED"):
+        rt.render(batch_samples=1, on_progress=lambda f: True)
+    sums, done = rt.checkpoint()
+    assert done == 4
+    rt2 = _rtow(64, 36, 16)
+    rt2.sum_order = capi.RT_SUM_SAMPLE_ORDER
+    assert np.array_equal(rt2.render(want=("mean",), resume=(sums, done), batch_samples=1)["mean"], full["mean"])
+
+
 def test_max_depth_zero_is_black(gpu):
     rt = _rtow(32, 18, 4)
     rt.max_bounces = -1        # truthy in JS: rayColor(ray, -1) returns 0 immediately
