@@ -79,9 +79,31 @@ template <class R> RT_HD R dot(V3<R> a, V3<R> b) { return a.x * b.x + a.y * b.y 
 template <class R> RT_HD V3<R> cross(V3<R> a, V3<R> b) {
     return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
+// RT_DIV_RCP (A/B): a vector divided by one scalar s as three Markstein corrections from y = RN(1/s)
+// instead of three IEEE divisions: q0 = RN(x y), e = x - q0 s exactly (FMA), RN(q0 + e y) = RN(x / s)
+// when nothing under- or overflows (Markstein's theorem; 2e8 random binary64 pairs bit-identical to the
+// division on the host).  Guarded: outside 2^-900 <= |x|, 2^-400 <= |s| <= 2^400 (binary32: 2^-100,
+// 2^-40 .. 2^40) — zero components included — the plain divisions run.
+#ifndef RT_DIV_RCP
+#define RT_DIV_RCP 0
+#endif
+template <class R> RT_HD V3<R> vdiv_rcp(V3<R> a, R s, R y) {
+    const R xmin = sizeof(R) == 8 ? (R)0x1p-900 : (R)0x1p-100;
+    const R smin = sizeof(R) == 8 ? (R)0x1p-400 : (R)0x1p-40, smax = sizeof(R) == 8 ? (R)0x1p400 : (R)0x1p40;
+    const R as = fabs(s);
+    if (fabs(a.x) >= xmin && fabs(a.y) >= xmin && fabs(a.z) >= xmin && as >= smin && as <= smax) {
+        auto q = [&](R x) { const R q0 = x * y; return fma(fma(-q0, s, x), y, q0); };
+        return {q(a.x), q(a.y), q(a.z)};
+    }
+    return vdiv(a, s);
+}
 template <class R> RT_HD V3<R> normalize(V3<R> a) {          // math.js:18
     R l = sqrt(a.x * a.x + a.y * a.y + a.z * a.z);
+#if RT_DIV_RCP
+    return l > (R)0 ? vdiv_rcp(a, l, (R)1 / l) : mk<R>(0, 0, 0);
+#else
     return l > (R)0 ? vdiv(a, l) : mk<R>(0, 0, 0);
+#endif
 }
 template <class R> RT_HD V3<R> reflect(V3<R> a, V3<R> n) {   // math.js:19
     return a - n * ((R)2 * dot(a, n));
@@ -98,8 +120,9 @@ struct SphereFilter { float cx, cy, cz, r2p; };
 template <class R> struct PlaneRec { R px, py, pz, nx, ny, nz; };
 template <class R> struct BoxRec { R mnx, mny, mnz, mxx, mxy, mxz; };
 template <class R> struct TriRec { R v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z, nx, ny, nz; };  // e1=v1-v0, e2=v2-v0
-// A material in 40 B (binary64): c = albedo (Lambertian, Metal) or emission = color * intensity
-// (Emissive), p = roughness (Metal) or refraction index (Dielectric) — a hit reads one record per segment
+// A material in 40 B (binary64): c = albedo (Lambertian, Metal), emission = color * intensity
+// (Emissive) or, for a Dielectric, {1 / index, Schlick r0 of the front face, of the back face}; p =
+// roughness (Metal) or refraction index (Dielectric) — a hit reads one record per segment
 template <class R> struct MatRec { int type, pad; R c[3]; R p; };
 // BVH leaf records in leaf order: everything one primitive test and its acceptance need (the
 // binary32 filter, the R-precision geometry, World index, World.objects index, material) in one
@@ -134,6 +157,7 @@ struct SceneView {
     const SphereFilter* sphere_filter;   // f64 mode: binary32 pre-filter records (same order)
     int num_spheres;
     const R* sphere_r;             // radius (normal = (p - c) / r, geometry.js:34)
+    const R* sphere_inv_r;         // RN(1 / radius) in R (RT_DIV_RCP)
     const PlaneRec<R>* planes;
     const BoxRec<R>* boxes;
     const TriRec<R>* tris;
@@ -933,7 +957,11 @@ RT_HD Hit<R> hit_record(const SceneView<R>& sc, V3<R> o, V3<R> d, const Closest<
     h.mat = c.mat;
     if (c.kind == HIT_SPHERE) {
         const SphereRec<R> s = sc.spheres[c.idx];
+#if RT_DIV_RCP
+        set_face(h, d, vdiv_rcp(h.p - mk(s.cx, s.cy, s.cz), sc.sphere_r[c.idx], sc.sphere_inv_r[c.idx]));
+#else
         set_face(h, d, vdiv(h.p - mk(s.cx, s.cy, s.cz), sc.sphere_r[c.idx]));
+#endif
     } else if (c.kind == HIT_PLANE) {
         const PlaneRec<R> p = sc.planes[c.idx];
         set_face(h, d, mk(p.nx, p.ny, p.nz));

@@ -88,7 +88,7 @@ struct DeviceScene {
     DevBuf<Run> runs;
     DevBuf<SphereRec<R>> spheres;
     DevBuf<SphereFilter> sphere_filter;
-    DevBuf<R> sphere_r;
+    DevBuf<R> sphere_r, sphere_inv_r;
     DevBuf<PlaneRec<R>> planes;
     DevBuf<BoxRec<R>> boxes;
     DevBuf<TriRec<R>> tris;
@@ -104,7 +104,7 @@ struct DeviceScene {
     DevBuf<SphereLeaf<R>> grid_leaf;
     SceneView<R> view{};
     void release() {
-        runs.release(); spheres.release(); sphere_filter.release(); sphere_r.release(); planes.release(); boxes.release(); tris.release();
+        runs.release(); spheres.release(); sphere_filter.release(); sphere_r.release(); sphere_inv_r.release(); planes.release(); boxes.release(); tris.release();
         sphere_mat.release(); plane_mat.release(); box_mat.release(); tri_mat.release(); perm.release(); mats.release();
         plane_obj.release(); box_obj.release(); sphere_nodes.release(); tri_nodes.release(); bvh_sphere_leaf.release();
         bvh_tri_leaf.release(); big_sphere_leaf.release();
@@ -118,7 +118,7 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     make_records(hs, d, rec);
     hipError_t e = hipSuccess;
 #define UP(buf, vec) if (e == hipSuccess) e = upload(ds.buf, vec)
-    UP(runs, hs.runs); UP(spheres, rec.spheres); UP(sphere_filter, rec.sphere_filter); UP(sphere_r, rec.sphere_r); UP(planes, rec.planes);
+    UP(runs, hs.runs); UP(spheres, rec.spheres); UP(sphere_filter, rec.sphere_filter); UP(sphere_r, rec.sphere_r); UP(sphere_inv_r, rec.sphere_inv_r); UP(planes, rec.planes);
     UP(boxes, rec.boxes); UP(tris, rec.tris); UP(sphere_mat, hs.sphere_mat); UP(plane_mat, hs.plane_mat);
     UP(box_mat, hs.box_mat); UP(tri_mat, hs.tri_mat); UP(perm, rec.perm); UP(mats, rec.mats);
     UP(plane_obj, hs.plane_obj); UP(box_obj, hs.box_obj); UP(sphere_nodes, hs.sphere_bvh); UP(tri_nodes, hs.tri_bvh);
@@ -128,7 +128,7 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     if (e != hipSuccess) return fail(RT_ERR_DEVICE, "scene upload: %s", hipGetErrorString(e));
     SceneView<R>& v = ds.view;
     v.runs = ds.runs.p;
-    v.spheres = ds.spheres.p; v.sphere_filter = ds.sphere_filter.p; v.sphere_r = ds.sphere_r.p; v.planes = ds.planes.p; v.boxes = ds.boxes.p;
+    v.spheres = ds.spheres.p; v.sphere_filter = ds.sphere_filter.p; v.sphere_r = ds.sphere_r.p; v.sphere_inv_r = ds.sphere_inv_r.p; v.planes = ds.planes.p; v.boxes = ds.boxes.p;
     v.tris = ds.tris.p; v.sphere_mat = ds.sphere_mat.p; v.plane_mat = ds.plane_mat.p; v.box_mat = ds.box_mat.p;
     v.tri_mat = ds.tri_mat.p; v.mats = ds.mats.p; v.perm = ds.perm.p;
     v.plane_obj = ds.plane_obj.p; v.box_obj = ds.box_obj.p; v.sphere_nodes = ds.sphere_nodes.p; v.tri_nodes = ds.tri_nodes.p;

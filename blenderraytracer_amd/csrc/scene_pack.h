@@ -521,7 +521,7 @@ template <class R>
 struct HostRecords {
     std::vector<SphereRec<R>> spheres;
     std::vector<SphereFilter> sphere_filter;
-    std::vector<R> sphere_r;
+    std::vector<R> sphere_r, sphere_inv_r;
     std::vector<PlaneRec<R>> planes;
     std::vector<BoxRec<R>> boxes;
     std::vector<TriRec<R>> tris;
@@ -545,6 +545,8 @@ void make_records(const HostScene& hs, const rt_scene_desc& d, HostRecords<R>& o
         out.spheres[i] = SphereRec<R>{(R)s[0], (R)s[1], (R)s[2], sizeof(R) == 8 ? (R)s[3] : r * r};
     }
     out.sphere_r.assign(hs.sphere_r.begin(), hs.sphere_r.end());
+    out.sphere_inv_r.resize(out.sphere_r.size());
+    for (size_t i = 0; i < out.sphere_r.size(); ++i) out.sphere_inv_r[i] = (R)1 / out.sphere_r[i];
     out.sphere_filter.resize(hs.sphere_r.size());
     for (size_t i = 0; i < out.sphere_filter.size(); ++i) {
         const double* s = &hs.spheres[4 * i];
@@ -576,6 +578,16 @@ void make_records(const HostScene& hs, const rt_scene_desc& d, HostRecords<R>& o
         const double* c = m.type == RT_MAT_EMISSIVE ? m.emission : m.albedo;
         for (int k = 0; k < 3; ++k) r.c[k] = (R)c[k];
         r.p = (R)(m.type == RT_MAT_METAL ? m.roughness : m.ior);
+        if (m.type == RT_MAT_DIELECTRIC) {
+            // the two refraction ratios' values that Dielectric.scatter derives from the index alone,
+            // in R arithmetic exactly as the kernel would (materials.js:53, :79-80): c[0] = 1 / ior (the
+            // front face's ratio), c[1] / c[2] = Schlick's r0 for the front / back face's ratio
+            const R ior = r.p, inv = (R)1 / ior;
+            R f = ((R)1 - inv) / ((R)1 + inv), bk = ((R)1 - ior) / ((R)1 + ior);
+            r.c[0] = inv;
+            r.c[1] = f * f;
+            r.c[2] = bk * bk;
+        }
         out.mats[i] = r;
     }
     out.perm.assign(d.perm, d.perm + 512);
@@ -663,6 +675,7 @@ inline void choose_walk(HostScene& hs, const rt_scene_desc& d) {
     SceneView<double> v{};
     v.runs = hs.runs.data();
     v.spheres = rec.spheres.data(); v.sphere_filter = rec.sphere_filter.data(); v.sphere_r = rec.sphere_r.data();
+    v.sphere_inv_r = rec.sphere_inv_r.data();
     v.planes = rec.planes.data(); v.boxes = rec.boxes.data(); v.tris = rec.tris.data();
     v.sphere_mat = hs.sphere_mat.data(); v.plane_mat = hs.plane_mat.data(); v.box_mat = hs.box_mat.data();
     v.tri_mat = hs.tri_mat.data(); v.mats = rec.mats.data(); v.perm = rec.perm.data();

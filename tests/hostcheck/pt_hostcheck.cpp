@@ -22,7 +22,7 @@ struct HostView {
         choose_walk(hs, *d);
         make_records(hs, *d, rec);
         v.runs = hs.runs.data();
-        v.spheres = rec.spheres.data(); v.sphere_filter = rec.sphere_filter.data(); v.sphere_r = rec.sphere_r.data(); v.planes = rec.planes.data();
+        v.spheres = rec.spheres.data(); v.sphere_filter = rec.sphere_filter.data(); v.sphere_r = rec.sphere_r.data(); v.sphere_inv_r = rec.sphere_inv_r.data(); v.planes = rec.planes.data();
         v.boxes = rec.boxes.data(); v.tris = rec.tris.data(); v.sphere_mat = hs.sphere_mat.data();
         v.plane_mat = hs.plane_mat.data(); v.box_mat = hs.box_mat.data(); v.tri_mat = hs.tri_mat.data();
         v.mats = rec.mats.data(); v.perm = rec.perm.data();
