@@ -211,9 +211,6 @@ constexpr bool parks() { return RT_PARK != 0 && sizeof(R) == 8 && uses_stack<ACC
 #ifndef RT_DEFER_REGEN
 #define RT_DEFER_REGEN 16
 #endif
-#ifndef RT_DEFER_DIEL
-#define RT_DEFER_DIEL 0
-#endif
 
 // CANCEL: the launch carries a cancel word (progressive renders, Counters::cancel); the instantiation
 // without it holds no polling code (the poll's code alone cost 1.4 % on RTOW)
@@ -399,32 +396,9 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
     bool live = (uint32_t)lane < total;
     if (live) begin_item((uint32_t)lane);
     bool waiting = false;                     // as trace_pool_kernel (RT_DEFER_REGEN)
-#if RT_DEFER_DIEL
-    // A/B: a lane whose segment hit a Dielectric parks its hit until RT_DEFER_DIEL lanes are parked
-    // (or none traces), and the parked lanes then shade together (the dielectric branch otherwise runs
-    // for the one or two lanes that hit glass in an iteration)
-    bool parked = false;
-    Closest<R> c{};
-#endif
     while (live) {                            // lanes only ever leave this loop, so every live lane
         const uint64_t t0 = RT_TICK();        // has seen every update of `next`
         if (!waiting) {
-#if RT_DEFER_DIEL
-            if (!parked) {
-                c = closest_hit_acc<R, ACC>(sc, o, d, res.work, stk);
-                ++res.segments;
-                ++isegs;
-                parked = c.kind != HIT_NONE && (lmats ? lmats[c.mat].type : sc.mats[c.mat].type) == 2;
-            }
-            const uint64_t pm = __ballot(parked);
-            const bool shade = !parked || __popcll(pm) >= RT_DEFER_DIEL || __ballot(!parked) == 0;
-            const uint64_t t1 = RT_TICK();
-            V3<R> L;
-            if (shade) {
-                parked = false;
-                waiting = shade_segment(sc, c, o, d, T, depth, g, L, lmats);
-            }
-#else
             const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, res.work, stk);
             const uint64_t t1 = RT_TICK();
             if (RT_PROFILE) res.cyc[0] += t1 - t0;
@@ -432,7 +406,6 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
             ++isegs;
             V3<R> L;
             waiting = shade_segment(sc, c, o, d, T, depth, g, L, lmats);
-#endif
             if (RT_PROFILE) res.cyc[1] += RT_TICK() - t1;
             if (waiting) {
                 if (COUNT) {
