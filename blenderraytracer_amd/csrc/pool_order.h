@@ -1,0 +1,68 @@
+// pool_order.h — the sample pool's 8x8 tiles and the order in which its (tile, chunk) items are
+// visited (pt_trace.hip).  Host-and-device code: tests/hostcheck enumerates the order on the CPU
+// (tests/test_pool_order.py checks that it is a permutation).
+#pragma once
+#include "pt_path.h"
+
+namespace rt {
+
+// 8x8 tile `tile` of the crop: origin, valid width and valid pixel count (edge tiles are ragged)
+struct Tile { int x0, y0, vw, nv; };
+RT_HD Tile tile_of(const ImageParams& im, int tile) {
+    const int tiles_x = (im.cw + 7) / 8;
+    Tile t;
+    t.x0 = (tile % tiles_x) * 8;
+    t.y0 = (tile / tiles_x) * 8;
+    t.vw = min(8, im.cw - t.x0);
+    t.nv = t.vw * min(8, im.ch - t.y0);
+    return t;
+}
+
+// Visiting order of the pool's (tile, chunk) items.  It is a permutation only: each item is traced as
+// before and its partials stay at item = chunk * tiles + tile, so the sums are unchanged bit for bit.
+// RT_TILE_BLOCK = S: within a chunk the tiles are taken in blocks of S x S tiles (raster order inside
+// a block, blocks in raster order), so the items in flight cover compact screen regions rather than
+// full-width bands.  RT_XCD_RUN = K (one-wave pool kernel): workgroups b, b + 8, b + 16, ... share an
+// XCD (dispatch deals workgroups round-robin over the 8 XCDs); they take K consecutive positions of the
+// order, so each XCD's L2 serves its own screen region instead of all eight serving the same band.
+#ifndef RT_TILE_BLOCK
+#define RT_TILE_BLOCK 1
+#endif
+#ifndef RT_XCD_RUN
+#define RT_XCD_RUN 1024          // mesh50k +2.8 %, tile blocks ±0 on top
+#endif
+RT_HD int tile_at(const ImageParams& im, int t) {
+    constexpr int S = RT_TILE_BLOCK;
+    if constexpr (S <= 1) {
+        return t;
+    } else {
+        const int tiles_x = (im.cw + 7) / 8, tiles_y = (im.ch + 7) / 8;
+        const int band = t / (S * tiles_x);
+        const int rows = min(S, tiles_y - band * S);       // the last band may be shorter
+        const int o = t - band * S * tiles_x;
+        const int c = o / (S * rows);                      // every block before the last is S wide
+        const int oo = o - c * S * rows;
+        const int w = min(S, tiles_x - c * S);
+        const int r = oo / w;
+        return (band * S + r) * tiles_x + c * S + (oo - r * w);
+    }
+}
+// position in the visiting order of one-wave workgroup b of a launch of n workgroups
+RT_HD unsigned pool_position(unsigned b, unsigned n) {
+    constexpr unsigned K = RT_XCD_RUN;
+    if constexpr (K == 0) {
+        return b;
+    } else {
+        const unsigned g = b / (8 * K), r = b - g * 8 * K;
+        if ((g + 1) * 8 * K > n) return b;                 // the last, partial group keeps its order
+        return g * 8 * K + (r & 7) * K + (r >> 3);
+    }
+}
+// item (chunk * tiles + tile) at position p of the visiting order
+RT_HD unsigned item_at(const ImageParams& im, unsigned p, int tiles) {
+    if constexpr (RT_TILE_BLOCK <= 1) return p;
+    const unsigned ci = p / (unsigned)tiles;
+    return ci * (unsigned)tiles + (unsigned)tile_at(im, (int)(p - ci * (unsigned)tiles));
+}
+
+}  // namespace rt

@@ -17,6 +17,7 @@
 #include <cstring>
 
 #include "pt_launch.h"
+#include "pool_order.h"
 
 namespace rt {
 
@@ -122,18 +123,6 @@ __device__ __forceinline__ bool cancel_requested(const Counters& c, unsigned cop
 // this batch leaves items untraced: its partials must not be reduced (one lane writes)
 __device__ __forceinline__ void mark_aborted(const Counters& c) {
     __hip_atomic_store(c.aborted, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// 8x8 tile `tile` of the crop: origin, valid width and valid pixel count (edge tiles are ragged)
-struct Tile { int x0, y0, vw, nv; };
-__device__ __forceinline__ Tile tile_of(const ImageParams& im, int tile) {
-    const int tiles_x = (im.cw + 7) / 8;
-    Tile t;
-    t.x0 = (tile % tiles_x) * 8;
-    t.y0 = (tile / tiles_x) * 8;
-    t.vw = min(8, im.cw - t.x0);
-    t.nv = t.vw * min(8, im.ch - t.y0);
-    return t;
 }
 
 // ---- lane-per-pixel kernel (RT_SAMPLE_POOL=0) ----
@@ -254,7 +243,8 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
             return;
         }
     }
-    const int ci = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+    const unsigned item = item_at(im, pool_position(blockIdx.x, gridDim.x), tiles);
+    const int ci = item / tiles, tile = item % tiles;
     const Tile tl = tile_of(im, tile);
     const int vw = tl.vw, nv = tl.nv;
     const int sb = im.s_begin + ci * chunk, se = min(im.s_end, sb + chunk);
@@ -340,7 +330,7 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
     __syncthreads();
     if (lane < nv) {
         if (part) {
-            double* p = part + ((size_t)blockIdx.x * 3) * 64 + lane;     // blockIdx = chunk * tiles + tile
+            double* p = part + ((size_t)item * 3) * 64 + lane;           // item = chunk * tiles + tile
             p[0] = acc[lane];
             p[64] = acc[64 + lane];
             p[128] = acc[128 + lane];
@@ -361,11 +351,12 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
 // on RTOW binary64, from a different register allocation.)
 template <class R, bool COUNT, int ACC>
 __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __restrict__ part, const int tiles,
-                                          const int chunk, const unsigned item, double* acc, BvhStack stk,
+                                          const int chunk, const unsigned pos, double* acc, BvhStack stk,
                                           PixelResult& res, const int lane, const MatRec<R>* lmats = nullptr) {
     const ImageParams& im = args.im;
     const SceneView<R>& sc = args.sc;
-    const int ci = item / tiles, tile = item % tiles;     // (unsigned, as blockIdx.x)
+    const unsigned item = item_at(im, pos, tiles);       // pos: the queue's position
+    const int ci = item / tiles, tile = item % tiles;
     const Tile tl = tile_of(im, tile);
     const int vw = tl.vw, nv = tl.nv;
     const int sb = im.s_begin + ci * chunk, se = min(im.s_end, sb + chunk);

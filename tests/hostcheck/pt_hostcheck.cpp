@@ -6,6 +6,7 @@
 
 #include "../../blenderraytracer_amd/csrc/pt_path.h"
 #include "../../blenderraytracer_amd/csrc/scene_pack.h"
+#include "../../blenderraytracer_amd/csrc/pool_order.h"
 
 using namespace rt;
 
@@ -347,4 +348,20 @@ extern "C" int ptc_grid_info(const rt_scene_desc* d, int* n3, long long* regs, i
     *regs = (long long)hv.hs.grid_ids.size();
     *use_grid = hv.hs.use_grid ? 1 : 0;
     return 0;
+}
+
+// The sample pool's visiting order (pool_order.h, TEST TOOL): out[b] = the item (chunk * tiles + tile)
+// that one-wave workgroup b of a cw x ch x `chunks` launch traces (one_wave), or that queue position b
+// of the LDS kernel takes; params = {RT_TILE_BLOCK, RT_XCD_RUN, tiles}
+extern "C" long long ptc_pool_order(int cw, int ch, int chunks, int one_wave, unsigned* out, int* params) {
+    ImageParams im{};
+    im.cw = cw;
+    im.ch = ch;
+    const int tiles = ((cw + 7) / 8) * ((ch + 7) / 8);
+    const unsigned n = (unsigned)tiles * (unsigned)chunks;
+    for (unsigned b = 0; b < n; ++b) out[b] = item_at(im, one_wave ? pool_position(b, n) : b, tiles);
+    params[0] = RT_TILE_BLOCK;
+    params[1] = RT_XCD_RUN;
+    params[2] = tiles;
+    return n;
 }

@@ -11,7 +11,8 @@ from blenderraytracer_amd import capi
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "hostcheck", "pt_hostcheck.cpp")
-DEPS = [SRC] + [os.path.join(ROOT, "blenderraytracer_amd", "csrc", f) for f in ("pt_core.h", "pt_path.h", "scene_pack.h")]
+DEPS = [SRC] + [os.path.join(ROOT, "blenderraytracer_amd", "csrc", f) for f in ("pt_core.h", "pt_path.h", "scene_pack.h",
+                                                                          "pool_order.h")]
 LIB = os.path.join(HERE, "hostcheck", "_build", "libpt_hostcheck.so")
 _lib = None
 
@@ -124,3 +125,18 @@ def render(packed, settings, L=None):
                           segs.ctypes.data_as(C.POINTER(C.c_uint32)), draws.ctypes.data_as(C.POINTER(C.c_uint32)))
     assert rc == 0
     return {"mean": s / settings.samples, "segments": segs, "draws": draws}
+
+
+def pool_order(cw, ch, chunks, one_wave=True):
+    """The pool's visiting order (pool_order.h): (items by workgroup / queue position, RT_TILE_BLOCK,
+    RT_XCD_RUN, tiles)."""
+    import numpy as np
+    L = lib()
+    L.ptc_pool_order.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_int)]
+    L.ptc_pool_order.restype = C.c_longlong
+    tiles = ((cw + 7) // 8) * ((ch + 7) // 8)
+    out = np.zeros(tiles * chunks, dtype=np.uint32)
+    par = (C.c_int * 3)()
+    n = L.ptc_pool_order(cw, ch, chunks, int(one_wave), out.ctypes.data_as(C.POINTER(C.c_uint32)), par)
+    assert n == tiles * chunks
+    return out, par[0], par[1], par[2]

@@ -1,0 +1,56 @@
+"""The sample pool's item visiting order (blenderraytracer_amd/csrc/pool_order.h), enumerated by the
+kernel's own header code on the CPU (tests/hostcheck): it must be a permutation of the items
+(chunk * tiles + tile), so that every (tile, chunk) of the frame is traced exactly once and its
+partials land where reduce_kernel reads them — the order only decides which items are in flight
+together (tile blocks and XCD runs).  The GPU tests check the images themselves."""
+import numpy as np
+import pytest
+
+from tests import hostcheck_binding as hc
+
+SIZES = [(1920, 1080, 12), (1920, 1080, 1), (13, 7, 3), (8, 8, 1), (1, 1, 2), (100, 100, 3), (4096, 16, 2),
+         (9, 4000, 1), (515, 517, 5)]
+
+
+def _check(order, tiles, chunks):
+    n = tiles * chunks
+    assert order.shape == (n,)
+    assert np.array_equal(np.sort(order), np.arange(n, dtype=np.uint32)), "not a permutation"
+
+
+@pytest.mark.parametrize("cw,ch,chunks", SIZES)
+@pytest.mark.parametrize("one_wave", [True, False])
+def test_pool_order_is_a_permutation(cw, ch, chunks, one_wave):
+    order, s, k, tiles = hc.pool_order(cw, ch, chunks, one_wave)
+    _check(order, tiles, chunks)
+    if not one_wave or k == 0:
+        # the queue (and a launch without XCD runs) keeps chunk-major order: position p is in chunk p // tiles
+        assert np.array_equal(order // tiles, np.arange(tiles * chunks) // tiles)
+
+
+def test_pool_order_blocks_are_compact():
+    """With S x S tile blocks, every run of S*S positions inside a full block covers an S x S square."""
+    order, s, k, tiles = hc.pool_order(1920, 1080, 1, False)
+    if s <= 1:
+        pytest.skip("raster tile order in this build")
+    tx = (1920 + 7) // 8
+    xs, ys = order % tx, order // tx
+    blk = order[: s * s]
+    assert xs[: s * s].max() - xs[: s * s].min() == s - 1 and ys[: s * s].max() - ys[: s * s].min() == s - 1, blk
+
+
+@pytest.mark.parametrize("cw,ch,chunks", [(1920, 1080, 12), (13, 7, 3), (515, 517, 5), (8, 8, 1)])
+def test_pool_order_odd_parameters(cw, ch, chunks):
+    """A build with odd block and run sizes (3 x 3 tiles, runs of 5) is still a permutation, and its XCD
+    runs are contiguous: workgroups b, b + 8, ... of a full group take consecutive positions."""
+    L = hc.lib(("RT_TILE_BLOCK=3", "RT_XCD_RUN=5"))
+    import ctypes as C
+    L.ptc_pool_order.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_int)]
+    L.ptc_pool_order.restype = C.c_longlong
+    tiles = ((cw + 7) // 8) * ((ch + 7) // 8)
+    for one_wave in (1, 0):
+        out = np.zeros(tiles * chunks, dtype=np.uint32)
+        par = (C.c_int * 3)()
+        assert L.ptc_pool_order(cw, ch, chunks, one_wave, out.ctypes.data_as(C.POINTER(C.c_uint32)), par) == tiles * chunks
+        assert (par[0], par[1], par[2]) == (3, 5, tiles)
+        _check(out, tiles, chunks)
