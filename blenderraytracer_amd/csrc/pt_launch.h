@@ -29,6 +29,11 @@ struct Counters {
     // all of them: the waves' reads spread over many lines instead of queueing on one
     const uint32_t* cancel = nullptr;
     uint32_t* aborted = nullptr;
+    // fused batches (launch_trace_batches): per batch, the items done (device memory, zeroed before the
+    // launch) and the flag the item completing the batch raises (mapped host memory: the host enqueues
+    // the batch's reduce once it is set, and its gate commits the batch only if it is set)
+    uint32_t* batch_count = nullptr;
+    uint32_t* batch_flag = nullptr;
 };
 constexpr int kCancelCopies = 128, kCancelStride = 32;
 
@@ -44,6 +49,8 @@ struct ReduceGate {
     int32_t* done = nullptr;
     int32_t done_value = 0;
     uint32_t* skip = nullptr;
+    // a fused launch's batch: its completion flag (Counters::batch_flag; 0 = items left untraced)
+    const uint32_t* complete = nullptr;
 };
 
 // bvh: walk the BVHs (ACC_BVH_STACK, the ordered two-child walk), else World order (ACC_BRUTE).
@@ -64,6 +71,16 @@ hipError_t launch_trace_partials(const SceneView<R>& sc, const ImageParams& im, 
                                  double* part, size_t part_bytes, hipStream_t stream);
 hipError_t launch_reduce(const ImageParams& im, double* sum, const double* part, bool tri_bvh, hipStream_t stream,
                          const ReduceGate* gate = nullptr);
+// All batches of a progressive render in ONE pool launch (items batch-major in the pool's queue): batch
+// b = samples [im.s_begin + b * batch, ...) into part + b * fused_batch_doubles(...), each batch's items
+// signalled through c.batch_count / c.batch_flag.  The same items, chunks and partials as one
+// launch_trace_partials per batch, so launch_reduce of each batch's partials adds the same bits.
+template <class R>
+hipError_t launch_trace_batches(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh, int batch,
+                                double* part, size_t part_bytes, hipStream_t stream);
+// doubles of one batch's partials in a fused launch, and the items that complete it
+size_t fused_batch_doubles(int cw, int ch, int batch, bool tri_bvh, int chunk);
+uint32_t fused_batch_items(int cw, int ch, int batch, bool tri_bvh, int chunk);
 
 // World.hit of n rays (n x 6 doubles, device) -> t, kind, index (device): rt_closest_hits
 template <class R>
@@ -91,8 +108,10 @@ struct FinalizeParams {
     int tone_map;
     double exposure, gamma;
 };
+// preview: a running frame of a progressive render (RGBA8 only): preview_kernel, whose gamma pow is
+// binary32 (within one RGBA8 step of the exact frame on rare pixels; pt_trace.hip)
 hipError_t launch_finalize(const FinalizeParams& p, const double* sum, double* mean, float* post, uint8_t* rgba8,
-                           hipStream_t stream);
+                           hipStream_t stream, bool preview = false);
 hipError_t launch_denoise(int w, int h, double w1, double w2, const float* in, float* out, uint8_t* rgba8,
                           hipStream_t stream);
 

@@ -21,6 +21,10 @@ struct ImageParams {
     int aa_mode;
     uint32_t seedm;            // seed_mix(seed)
     int pool_chunk;            // samples per sample-pool wave (0: pool_chunk's rule for this launch's samples)
+    // fused batches (launch_trace_batches): the launch traces batches of batch_samples samples from
+    // s_begin, batch_chunks chunks each, batch-major (chunk index c of the launch = batch c / batch_chunks);
+    // 0: one batch
+    int batch_samples, batch_chunks;
 };
 
 // Stochastic AA offsets (ray-tracer.js:136-141): sqrt, cos and sin in binary64 are long code that

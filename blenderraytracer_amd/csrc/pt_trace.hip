@@ -113,6 +113,12 @@ __device__ __forceinline__ void add_totals(const Counters& c, const PixelResult&
 #ifndef RT_CANCEL_POLL
 #define RT_CANCEL_POLL 1          // A/B: 0 = the kernels never read the cancel word (the gates still run)
 #endif
+// The LDS pool kernel's wave 0 reads the cancel word before every RT_CANCEL_EVERY-th item of its own (a
+// read of mapped host memory stalls the wave for its PCIe round trip; config 3 in 16 fused batches:
+// every item +3.5 %), the workgroup's other waves read its LDS flag before every item
+#ifndef RT_CANCEL_EVERY
+#define RT_CANCEL_EVERY 4
+#endif
 // copy: the wave's copy of the word (Counters::cancel); one line read by every wave measured 50 us per
 // read (RTOW 16 progressive batches: +4.5 % kernel time), the reads of one line being serialized
 __device__ __forceinline__ bool cancel_requested(const Counters& c, unsigned copy) {
@@ -120,9 +126,41 @@ __device__ __forceinline__ bool cancel_requested(const Counters& c, unsigned cop
            __hip_atomic_load(const_cast<uint32_t*>(c.cancel) + (copy % kCancelCopies) * kCancelStride, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_SYSTEM) != 0;
 }
-// this batch leaves items untraced: its partials must not be reduced (one lane writes)
+// this batch leaves items untraced: its partials must not be reduced (one lane writes; a fused launch's
+// batches are committed by their completion flags instead, ReduceGate::complete)
 __device__ __forceinline__ void mark_aborted(const Counters& c) {
     __hip_atomic_store(c.aborted, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// (batch, chunk within it, first sample, end sample) of launch chunk gci (ImageParams::batch_chunks)
+struct ChunkRange { int b, ci, sb, se; };
+__device__ __forceinline__ ChunkRange chunk_range(const ImageParams& im, int gci, int chunk) {
+    ChunkRange r;
+    r.b = im.batch_chunks ? gci / im.batch_chunks : 0;
+    r.ci = gci - r.b * im.batch_chunks;
+    const int bs = im.s_begin + r.b * im.batch_samples;
+    r.sb = bs + r.ci * chunk;
+    r.se = min(im.batch_chunks ? min(im.s_end, bs + im.batch_samples) : im.s_end, r.sb + chunk);
+    return r;
+}
+
+// A chunk partial of a fused launch: stored through to memory (sc1: agent-scope store), since the
+// reduce that reads it runs while this launch is still going, on whatever XCD
+__device__ __forceinline__ void store_through(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The wave's item of a fused launch is done: once its partials' stores have completed (vmcnt(0), as
+// inline asm, which the compiler cannot drop), lane 0 counts the item for its batch, and the lane whose
+// count completes the batch raises the batch's flag in mapped host memory (the host then enqueues the
+// batch's reduce, a later kernel launch, so the reads need no acquire of their own)
+__device__ __forceinline__ void item_done(const Counters& c, int b, uint32_t batch_items, int lane) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+        const uint32_t k = __hip_atomic_fetch_add(c.batch_count + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k + 1 == batch_items) __hip_atomic_store(c.batch_flag + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // ---- lane-per-pixel kernel (RT_SAMPLE_POOL=0) ----
@@ -244,10 +282,11 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
         }
     }
     const unsigned item = item_at(im, pool_position(blockIdx.x, gridDim.x), tiles);
-    const int ci = item / tiles, tile = item % tiles;
+    const int tile = item % tiles;
+    const ChunkRange cr = chunk_range(im, (int)(item / tiles), chunk);
     const Tile tl = tile_of(im, tile);
     const int vw = tl.vw, nv = tl.nv;
-    const int sb = im.s_begin + ci * chunk, se = min(im.s_end, sb + chunk);
+    const int sb = cr.sb, se = cr.se;
     const uint32_t total = (uint32_t)nv * (uint32_t)max(0, se - sb);
     PixelResult res{0, 0, {0, 0, 0}, {0, 0, 0}};
     // the lane's current item: pixel m of the tile = (i, j) with key pkey at crop index q, sample s
@@ -331,9 +370,15 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
     if (lane < nv) {
         if (part) {
             double* p = part + ((size_t)item * 3) * 64 + lane;           // item = chunk * tiles + tile
-            p[0] = acc[lane];
-            p[64] = acc[64 + lane];
-            p[128] = acc[128 + lane];
+            if (args.c.batch_count) {
+                store_through(p, acc[lane]);
+                store_through(p + 64, acc[64 + lane]);
+                store_through(p + 128, acc[128 + lane]);
+            } else {
+                p[0] = acc[lane];
+                p[64] = acc[64 + lane];
+                p[128] = acc[128 + lane];
+            }
         } else {                                  // the launch's only chunk: this wave owns the pixels
             const size_t qq = (size_t)(tl.y0 + lane / vw) * im.cw + (tl.x0 + lane % vw);
             args.c.sum[3 * qq] += acc[lane];
@@ -341,6 +386,7 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
             args.c.sum[3 * qq + 2] += acc[128 + lane];
         }
     }
+    if (args.c.batch_count) item_done(args.c, cr.b, (uint32_t)(im.batch_chunks * tiles), lane);
     add_totals<ACC>(args.c, res, lane);
 }
 
@@ -356,10 +402,11 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
     const ImageParams& im = args.im;
     const SceneView<R>& sc = args.sc;
     const unsigned item = item_at(im, pos, tiles);       // pos: the queue's position
-    const int ci = item / tiles, tile = item % tiles;
+    const int tile = item % tiles;
+    const ChunkRange cr = chunk_range(im, (int)(item / tiles), chunk);
     const Tile tl = tile_of(im, tile);
     const int vw = tl.vw, nv = tl.nv;
-    const int sb = im.s_begin + ci * chunk, se = min(im.s_end, sb + chunk);
+    const int sb = cr.sb, se = cr.se;
     const uint32_t total = (uint32_t)nv * (uint32_t)max(0, se - sb);
     // the lane's current item: pixel m of the tile = (i, j) with key pkey at crop index q, sample s
     int i = 0, j = 0, s = 0, depth = 0;
@@ -427,9 +474,15 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
     if (lane < nv) {
         if (part) {
             double* p = part + ((size_t)item * 3) * 64 + lane;           // item = chunk * tiles + tile
-            p[0] = acc[lane];
-            p[64] = acc[64 + lane];
-            p[128] = acc[128 + lane];
+            if (args.c.batch_count) {
+                store_through(p, acc[lane]);
+                store_through(p + 64, acc[64 + lane]);
+                store_through(p + 128, acc[128 + lane]);
+            } else {
+                p[0] = acc[lane];
+                p[64] = acc[64 + lane];
+                p[128] = acc[128 + lane];
+            }
         } else {                                  // the launch's only chunk: this wave owns the pixels
             const size_t qq = (size_t)(tl.y0 + lane / vw) * im.cw + (tl.x0 + lane % vw);
             args.c.sum[3 * qq] += acc[lane];
@@ -437,6 +490,7 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
             args.c.sum[3 * qq + 2] += acc[128 + lane];
         }
     }
+    if (args.c.batch_count) item_done(args.c, cr.b, (uint32_t)(im.batch_chunks * tiles), lane);
     acc[lane] = 0;                            // the wave's next item starts from zero partials
     acc[64 + lane] = 0;
     acc[128 + lane] = 0;
@@ -537,12 +591,13 @@ void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, c
     __syncthreads();
     uint32_t* queue = g_pool_queue + 2 * qi;
     PixelResult res{0, 0, {0, 0, 0}, {0, 0, 0}};
+    unsigned taken = 0;                       // CANCEL: items this wave has taken
     for (;;) {
         uint32_t it = 0;
         int stop = 0;
         if (lane == 0) {
             if constexpr (CANCEL) {
-                if (wave == 0 && cancel_requested(args.c, blockIdx.x))
+                if (wave == 0 && taken++ % RT_CANCEL_EVERY == 0 && cancel_requested(args.c, blockIdx.x))
                     __hip_atomic_store(&stop_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 stop = (int)__hip_atomic_load(&stop_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
@@ -594,7 +649,8 @@ __global__ __launch_bounds__(64) void reduce_gate_kernel(const ReduceGate g) {
     if (threadIdx.x != 0) return;
     const uint32_t a = __hip_atomic_load(const_cast<uint32_t*>(g.aborted), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint32_t s = __hip_atomic_load(g.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint32_t skip = (a | s) ? 1u : 0u;
+    const uint32_t f = g.complete ? __hip_atomic_load(g.complete, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 1u;
+    const uint32_t skip = (a | s) || !f ? 1u : 0u;
     *g.skip = skip;
     if (skip) __hip_atomic_store(g.stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     else __hip_atomic_store(g.done, g.done_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -868,6 +924,43 @@ template hipError_t launch_trace_partials<double>(const SceneView<double>&, cons
 template hipError_t launch_trace_partials<float>(const SceneView<float>&, const ImageParams&, const Counters&, bool,
                                                  double*, size_t, hipStream_t);
 
+size_t fused_batch_doubles(int cw, int ch, int batch, bool tri_bvh, int chunk) {
+    return pool_plan(cw, ch, batch, tri_bvh, chunk).part_bytes / sizeof(double);
+}
+uint32_t fused_batch_items(int cw, int ch, int batch, bool tri_bvh, int chunk) {
+    const PoolPlan p = pool_plan(cw, ch, batch, tri_bvh, chunk);
+    return (uint32_t)((size_t)p.tiles * p.chunks);
+}
+
+template <class R>
+hipError_t launch_trace_batches(const SceneView<R>& sc, const ImageParams& im0, const Counters& c, bool bvh, int batch,
+                                double* part, size_t part_bytes, hipStream_t stream) {
+    if (im0.cw <= 0 || im0.ch <= 0 || im0.s_end <= im0.s_begin || batch <= 0) return hipSuccess;
+    const bool tri = sc.num_tri_nodes > 0;
+    const PoolPlan p = pool_plan(im0.cw, im0.ch, batch, tri, im0.pool_chunk);   // one batch's chunks
+    const int nb = (im0.s_end - im0.s_begin + batch - 1) / batch;
+    if (!part || !c.batch_count || !c.batch_flag || part_bytes < (size_t)nb * p.part_bytes) return hipErrorInvalidValue;
+    if ((long long)p.tiles * p.chunks * nb > 0x7FFFFFFFLL) return hipErrorInvalidConfiguration;
+    ImageParams im = im0;
+    im.pool_chunk = p.chunk;
+    im.batch_samples = batch;
+    im.batch_chunks = p.chunks;
+    const PoolPlan all{p.tiles, p.chunk, p.chunks * nb, (size_t)nb * p.part_bytes};
+    TraceArgs<R> a{sc, im, c};
+    const bool count = c.segs || c.draws;
+    if (!bvh) return launch_partials_acc<R, ACC_BRUTE>(a, count, all, part, stream);
+    const int mode = bvh_walk_mode(sc);
+    if (mode == ACC_BVH) return launch_partials_acc<R, ACC_BVH>(a, count, all, part, stream);
+    if (mode == ACC_BVH_SPHERES) return launch_partials_acc<R, ACC_BVH_SPHERES>(a, count, all, part, stream);
+    if (mode == ACC_GRID) return launch_partials_acc<R, ACC_GRID>(a, count, all, part, stream);
+    return launch_partials_acc<R, ACC_BVH_STACK>(a, count, all, part, stream);
+}
+
+template hipError_t launch_trace_batches<double>(const SceneView<double>&, const ImageParams&, const Counters&, bool, int,
+                                                 double*, size_t, hipStream_t);
+template hipError_t launch_trace_batches<float>(const SceneView<float>&, const ImageParams&, const Counters&, bool, int,
+                                                double*, size_t, hipStream_t);
+
 hipError_t launch_reduce(const ImageParams& im, double* sum, const double* part, bool tri_bvh, hipStream_t stream,
                          const ReduceGate* gate) {
     if (im.cw <= 0 || im.ch <= 0 || im.s_end <= im.s_begin) return hipSuccess;
@@ -990,6 +1083,16 @@ __device__ __forceinline__ uint8_t to_u8(double c) {
 }
 
 // one-wave workgroups, like reduce_kernel: the preview frames run beside trace waves
+// one channel of the epilogue: the mean times exposure, tone map, gamma (ray-tracer.js:216-235)
+__device__ __forceinline__ double post_channel(const FinalizeParams& p, double c, double inv_gamma) {
+    const double x = c * p.exposure;
+    double tm;
+    if (p.tone_map == 1) tm = js_max<double>(0.0, (x * (2.51 * x + 0.03)) / (x * (2.43 * x + 0.59) + 0.14));
+    else if (p.tone_map == 2) tm = x;
+    else tm = x / (1.0 + x);
+    return pow(js_max<double>(0.0, tm), inv_gamma);
+}
+
 __global__ __launch_bounds__(64) void finalize_kernel(const FinalizeParams p, const double* __restrict__ sum,
                                                        double* __restrict__ mean, float* __restrict__ post,
                                                        uint8_t* __restrict__ rgba8) {
@@ -999,13 +1102,7 @@ __global__ __launch_bounds__(64) void finalize_kernel(const FinalizeParams p, co
     const double inv_gamma = 1.0 / p.gamma;
     for (int k = 0; k < 3; ++k) c[k] = sum[3 * q + k] / (double)p.samples;
     if (mean) { mean[3 * q] = c[0]; mean[3 * q + 1] = c[1]; mean[3 * q + 2] = c[2]; }
-    for (int k = 0; k < 3; ++k) {
-        double x = c[k] * p.exposure, tm;
-        if (p.tone_map == 1) tm = js_max<double>(0.0, (x * (2.51 * x + 0.03)) / (x * (2.43 * x + 0.59) + 0.14));
-        else if (p.tone_map == 2) tm = x;
-        else tm = x / (1.0 + x);
-        g[k] = pow(js_max<double>(0.0, tm), inv_gamma);
-    }
+    for (int k = 0; k < 3; ++k) g[k] = post_channel(p, c[k], inv_gamma);
     if (post) *reinterpret_cast<float4*>(post + 4 * q) = make_float4((float)g[0], (float)g[1], (float)g[2], 1.0f);
     if (rgba8) {
         uchar4 o = make_uchar4(to_u8(g[0]), to_u8(g[1]), to_u8(g[2]), 255);
@@ -1013,10 +1110,38 @@ __global__ __launch_bounds__(64) void finalize_kernel(const FinalizeParams p, co
     }
 }
 
+// The running frame of a progressive render (RGBA8 only) in at most 32 VGPRs: while batches trace, the
+// trace waves hold 480 of a SIMD's 512 VGPRs (5 waves x 96), and finalize_kernel's 80-VGPR waves wait
+// for trace waves to exit (measured 0.2 - 7.5 ms per preview, delaying the next batches' reduces on the
+// same stream; a fused launch's waves never exit).  The binary64 pow alone needs 64 VGPRs, so the gamma
+// pow here is binary32 (28 VGPRs): the frame is within one RGBA8 step of finalize_kernel's on pixels
+// whose value lies within ~1e-7 of a rounding boundary.  The final frame and a cancelled render's frame
+// come from finalize_kernel.
+__global__ __launch_bounds__(64) void preview_kernel(const FinalizeParams p, const double* __restrict__ sum,
+                                                     uint8_t* __restrict__ rgba8) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= p.n) return;
+    const float inv_gamma = (float)(1.0 / p.gamma);
+    uint32_t o = 255u << 24;
+#pragma unroll 1
+    for (int k = 0; k < 3; ++k) {
+        const double x = sum[3 * q + k] / (double)p.samples * p.exposure;
+        double tm;
+        if (p.tone_map == 1) tm = js_max<double>(0.0, (x * (2.51 * x + 0.03)) / (x * (2.43 * x + 0.59) + 0.14));
+        else if (p.tone_map == 2) tm = x;
+        else tm = x / (1.0 + x);
+        o |= (uint32_t)to_u8((double)powf((float)js_max<double>(0.0, tm), inv_gamma)) << (8 * k);
+    }
+    *reinterpret_cast<uint32_t*>(rgba8 + 4 * q) = o;
+}
+
 hipError_t launch_finalize(const FinalizeParams& p, const double* sum, double* mean, float* post, uint8_t* rgba8,
-                           hipStream_t stream) {
+                           hipStream_t stream, bool preview) {
     if (p.n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(finalize_kernel, dim3((p.n + 63) / 64), dim3(64), 0, stream, p, sum, mean, post, rgba8);
+    if (preview && !mean && !post && rgba8)
+        hipLaunchKernelGGL(preview_kernel, dim3((p.n + 63) / 64), dim3(64), 0, stream, p, sum, rgba8);
+    else
+        hipLaunchKernelGGL(finalize_kernel, dim3((p.n + 63) / 64), dim3(64), 0, stream, p, sum, mean, post, rgba8);
     return hipGetLastError();
 }
 

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt_hip.h"
@@ -158,7 +159,12 @@ inline int lookahead(int devices) { return kSlots * std::max(1, devices); }
 // kCtlCancel: kCancelCopies copies of the cancel word, one per 128-B line (pt_launch.h).
 constexpr int kCtlStop = 1, kCtlDone = 2, kCtlAborted = 4;
 constexpr int kCtlCancel = 128;
-constexpr int kCtlWords = kCtlCancel + kCancelCopies * kCancelStride;
+// fused batches (render_impl): per batch, the flag its last item raises; two `aborted` words (the gates'
+// stand-in, never written; the skipping waves', never read)
+constexpr int kMaxFused = 64;
+constexpr int kCtlFlag = kCtlCancel + kCancelCopies * kCancelStride;
+constexpr int kCtlFusedAborted = kCtlFlag + kMaxFused;
+constexpr int kCtlWords = kCtlFusedAborted + 2;
 static_assert(kCtlAborted + kSlots * RT_MAX_DEVICES + kSlots <= kCtlCancel, "one aborted word per ring slot");
 inline uint32_t ctl_load(const uint32_t* ctl, int k) { return __atomic_load_n(ctl + k, __ATOMIC_SEQ_CST); }
 inline void ctl_store(uint32_t* ctl, int k, uint32_t v) { __atomic_store_n(ctl + k, v, __ATOMIC_SEQ_CST); }
@@ -190,6 +196,11 @@ struct DeviceState {
     DevBuf<double> part_more[kSlots - 1];   // partials of slots 1 ..
     hipEvent_t traced[kSlots] = {}, reduced[kSlots] = {}, setup_ev = nullptr;
     DevBuf<double>& slot_part(int j) { return j == 0 ? part : part_more[j - 1]; }
+    // fused batches (render_impl): every batch's chunk partials, the items done per batch, and the
+    // event recorded after the one launch on tstream[0]
+    DevBuf<double> fused_part;
+    DevBuf<uint32_t> fused_count;
+    hipEvent_t fused_done = nullptr;
 
     int init(int dev, const HostScene& hs, const rt_scene_desc& d) {
         device = dev;
@@ -208,6 +219,7 @@ struct DeviceState {
         for (int k = 0; k < kSlots && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&traced[k], hipEventDisableTiming);
         for (int k = 0; k < kSlots && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&reduced[k], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&setup_ev, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&fused_done, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&scratch_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&copy_ev, hipEventDisableTiming);
         if (e != hipSuccess) return fail(RT_ERR_DEVICE, "stream/event create: %s", hipGetErrorString(e));
@@ -224,8 +236,9 @@ struct DeviceState {
         s64.release();
         s32.release();
         sum.release(); segs.release(); draws.release(); total.release(); part.release(); gate_skip.release();
+        fused_part.release(); fused_count.release();
         for (DevBuf<double>& b : part_more) b.release();
-        for (hipEvent_t e : {ev[0], ev[1], setup_ev, scratch_ev, copy_ev})
+        for (hipEvent_t e : {ev[0], ev[1], setup_ev, scratch_ev, copy_ev, fused_done})
             if (e) (void)hipEventDestroy(e);
         for (int k = 0; k < kSlots; ++k) {
             if (traced[k]) (void)hipEventDestroy(traced[k]);
@@ -556,6 +569,35 @@ bool ensure_overlap_partials(DeviceState& ds, size_t bytes) {
     return true;
 }
 
+// Fused batches: the chunk partials of all `nb` batches of a render (`doubles` each) and their item
+// counters.  The partials budget is RT_FUSED_MB (default 8 GiB, at most 10 % of the free device
+// memory; config 3 in 16 batches needs 0.8 GB); false (no error) when they do not fit: the render then
+// launches its batches one by one.
+bool ensure_fused(DeviceState& ds, size_t doubles, int nb) {
+    const size_t bytes = doubles * (size_t)nb * sizeof(double);
+    if (bytes == 0) return false;
+    if (ds.fused_part.n * sizeof(double) < bytes) {
+        static size_t budget = 0;
+        if (!budget) {
+            const char* e = getenv("RT_FUSED_MB");
+            budget = (size_t)(e ? std::max(0LL, atoll(e)) : 8192LL) << 20;
+        }
+        size_t free_b = 0, total_b = 0, cap = budget;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = std::min(cap, (free_b + ds.fused_part.n * sizeof(double)) / 10);
+        if (bytes > cap) return false;
+        ds.fused_part.release();
+        if (ds.fused_part.ensure(bytes / sizeof(double)) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+    }
+    if (ds.fused_count.ensure((size_t)nb) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return true;
+}
+
 // A device state's scratch buffers (chunk partials, work totals) are shared by every call on it.  A
 // call on stream `st` first waits for the previous user of the scratch (possibly another stream:
 // rt_trace_device on a caller's stream, rt_render on the scene's own) and records the event again
@@ -873,11 +915,29 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     // the batches [0, k) for some k.  For batches reduced on one stream in batch order: one device, or
     // the whole-batch split.  The split of every batch over devices observes a cancel between batches.
     static const bool item_cancel = !(getenv("RT_ITEM_CANCEL") && getenv("RT_ITEM_CANCEL")[0] == '0');   // A/B runs
-    const bool gated = item_cancel && overlap && (nsh == 1 || whole);
+    static const bool fuse_env = !(getenv("RT_FUSED_BATCHES") && getenv("RT_FUSED_BATCHES")[0] == '0');   // A/B runs
+    // (RT_ITEM_CANCEL=0 with fused batches: the gates run, the kernels poll no cancel word — A/B only)
+    const bool gated = (item_cancel || (fuse_env && nsh == 1)) && overlap && (nsh == 1 || whole);
     if (gated) {
         HIP_TRY(hipSetDevice(h.device));
         HIP_TRY(h.gate_skip.ensure(1));
     }
+    // Fused batches (one device, overlapped gated batches): every batch in ONE pool launch, its items
+    // batch-major in the pool's queue (launch_trace_batches: the same items, chunks and partials as one
+    // launch per batch), and each batch's reduce enqueued by the host once the batch's last item has
+    // raised its flag — the persistent workgroups never drain between batches (16 batches of config 3
+    // drained for 3.5 % of the trace time).  The reduces (16 VGPRs) and the preview frames (binary32
+    // pow, 28 VGPRs) run beside the trace waves, which leave 32 of a SIMD's 512 VGPRs free.
+    int fchunk = 0;
+    size_t fdoubles = 0;
+    bool fused = fuse_env && gated && nsh == 1 && !whole && nb > 1 && nb <= kMaxFused && states[0] == &h;
+    if (fused) {
+        fchunk = batch_chunk(0, batch);
+        fdoubles = fused_batch_doubles(cw, ch, batch, sc->tri_bvh, fchunk);
+        HIP_TRY(hipSetDevice(h.device));
+        fused = ensure_fused(h, fdoubles, nb);
+    }
+    bool fused_launched = false;
     for (int k = 0; k < nsh; ++k) {
         DeviceState& ds = *states[k];
         HIP_TRY(hipSetDevice(ds.device));
@@ -957,9 +1017,11 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         ReduceGate gate;                          // gated: batch kb's cancel and commit words
         const ReduceGate* gp = nullptr;
         if (gated) {
-            const int w = kCtlAborted + kb % ring;
-            ctl_store(sc->ctl, w, 0);             // batch kb - ring, the slot's last user, has completed
+            // fused: the batch's flag commits it (a word no kernel writes stands in for `aborted`)
+            const int w = fused ? kCtlFusedAborted : kCtlAborted + kb % ring;
+            if (!fused) ctl_store(sc->ctl, w, 0);   // batch kb - ring, the slot's last user, has completed
             gate.aborted = sc->ctl_dev + w;
+            if (fused) gate.complete = sc->ctl_dev + kCtlFlag + kb;
             gate.stop = sc->ctl_dev + kCtlStop;
             gate.done = reinterpret_cast<int32_t*>(sc->ctl_dev + kCtlDone);
             gate.done_value = be;
@@ -968,11 +1030,45 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         }
         auto with_cancel = [&](Counters c) {
             if (gated) {
-                c.cancel = sc->ctl_dev + kCtlCancel;
+                if (item_cancel) c.cancel = sc->ctl_dev + kCtlCancel;
                 c.aborted = const_cast<uint32_t*>(gate.aborted);
             }
             return c;
         };
+        if (fused) {                              // the render's one launch, then batch kb's reduce
+            HIP_TRY(hipSetDevice(h.device));
+            const bool bvh = use_bvh(sc, s);
+            if (kb == 0) {
+                for (int k = 0; k < nb; ++k) ctl_store(sc->ctl, kCtlFlag + k, 0);
+                ctl_store(sc->ctl, kCtlFusedAborted, 0);
+                ctl_store(sc->ctl, kCtlFusedAborted + 1, 0);
+                HIP_TRY(hipMemsetAsync(h.fused_count.p, 0, nb * sizeof(uint32_t), h.tstream[0]));
+                Counters c = with_cancel(cs[0]);
+                c.aborted = sc->ctl_dev + kCtlFusedAborted + 1;   // written by skipping waves, read by no gate
+                c.batch_count = h.fused_count.p;
+                c.batch_flag = sc->ctl_dev + kCtlFlag;
+                ImageParams fi = im;
+                fi.s_begin = s0;
+                fi.s_end = s1;
+                fi.pool_chunk = fchunk;
+                const size_t fb = h.fused_part.n * sizeof(double);
+                HIP_TRY(s->precision == RT_PREC_F32
+                            ? launch_trace_batches<float>(h.s32.view, fi, c, bvh, batch, h.fused_part.p, fb, h.tstream[0])
+                            : launch_trace_batches<double>(h.s64.view, fi, c, bvh, batch, h.fused_part.p, fb, h.tstream[0]));
+                HIP_TRY(hipEventRecord(h.fused_done, h.tstream[0]));
+                fused_launched = true;
+            }
+            // the host waits for batch kb's flag; without it (a cancel: its items stay untraced) the
+            // accumulation stream waits for the launch to end, so the gate reads the final `aborted` words
+            while (!ctl_load(sc->ctl, kCtlFlag + kb) && !sc->cancel.load() && hipEventQuery(h.fused_done) == hipErrorNotReady)
+                std::this_thread::sleep_for(std::chrono::microseconds(20));
+            if (!ctl_load(sc->ctl, kCtlFlag + kb)) HIP_TRY(hipStreamWaitEvent(h.stream, h.fused_done, 0));
+            ImageParams bi = im;
+            bi.s_begin = b;
+            bi.s_end = be;
+            bi.pool_chunk = fchunk;
+            HIP_TRY(launch_reduce(bi, h.sum.p, h.fused_part.p + (size_t)kb * fdoubles, sc->tri_bvh, h.stream, gp));
+        }
         if (whole) {                              // the whole batch on one device, reduced on the home device
             const int k = kb % nsh, lj = kb / nsh, j = lj % kSlots;
             DeviceState& ds = *states[k];
@@ -985,7 +1081,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
             if (&ds == &h) HIP_TRY(trace_overlapped(sc, ds, s, bi, with_cancel(cs[k]), j, lj >= kSlots, gp));
             else if (int r = trace_replica(sc, ds, sc->merge[k], s, bi, with_cancel(cs[k]), j, gp)) return r;
         }
-        for (int k = 0; k < nsh && !whole; ++k) { // every shard's launches first: the devices run together
+        for (int k = 0; k < nsh && !whole && !fused; ++k) { // every shard's launches first: the devices run together
             DeviceState& ds = *states[k];
             ImageParams bi = im;
             shard_range(b, be, k, nsh, bi.s_begin, bi.s_end);
@@ -1002,7 +1098,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
             // hipMemcpyAsync here is a blit kernel that waits for wave slots behind the trace waves
             // (measured 7-15 ms per 8-MB frame while batches overlap)
             FinalizeParams fp{(int)n, be - base, s->tone_map, s->exposure, s->gamma};
-            HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview_dev[kb % ring], h.stream));
+            HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview_dev[kb % ring], h.stream, true));
         }
         HIP_TRY(hipEventRecord(sc->batch_done[kb % ring], h.stream));
         return RT_OK;
@@ -1036,7 +1132,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         return RT_OK;
     };
     for (int kb = 0; kb < nb && status == RT_OK; ++kb) {
-        if ((status = fill(kb + ahead + 1))) break;
+        if ((status = fill(kb + (fused ? 0 : ahead) + 1))) break;   // fused: enqueue(kb) waits for batch kb
         bool merged = true;
         if ((status = complete(kb, merged))) break;
         const int be = sc->ckpt_done;
@@ -1090,6 +1186,10 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
                 if (slots_used[k] & (1u << j)) HIP_TRY(hipStreamWaitEvent(ds->stream, ds->traced[j], 0));
         }
         if ((rc = merge_counters(sc, states, n, want_segs, want_draws))) return rc;
+    }
+    if (fused_launched) {                         // the launch's last waves (work totals) before the stats
+        HIP_TRY(hipSetDevice(h.device));
+        HIP_TRY(hipStreamWaitEvent(h.stream, h.fused_done, 0));
     }
     unsigned long long totals[kTotalSlots] = {};
     float kernel_ms = 0;

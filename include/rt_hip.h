@@ -190,8 +190,10 @@ typedef struct rt_output {
     uint8_t* preview_rgba8;   /* n*4, progressive display (ray-tracer.js:224-241 putImageData per row): with
                                  more than one sample batch, before every progress() call this buffer holds
                                  the RGBA8 frame of the samples traced so far (mean over those samples, tone
-                                 map, gamma; no denoise, like the reference's rows before its final pass).
-                                 After a cancel the buffer holds the frame of the checkpointed samples.  A batch
+                                 map, gamma; no denoise, like the reference's rows before its final pass;
+                                 the gamma pow of these running frames is binary32, so a pixel within ~1e-7 of
+                                 an RGBA8 rounding boundary may differ by one step from rgba8's exact frame).
+                                 After a cancel the buffer holds the exact frame of the checkpointed samples.  A batch
                                  whose successor has already finished when the host gets to it is skipped
                                  (the buffer keeps the previous frame until the newer one is copied) */
     int32_t* preview_samples; /* optional out: the samples (from sample_begin) in preview_rgba8's frame,

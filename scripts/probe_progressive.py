@@ -1,6 +1,6 @@
 """Progressive-render cost probe (DEV TOOL): config 3 as one batch and as 16 batches of 32 spp, each
 rendered `reps` times; prints the median kernel and wall time.
-usage: python scripts/probe_progressive.py [reps]"""
+usage: python scripts/probe_progressive.py [reps] [batch sizes, comma-separated; 0 = one batch]"""
 import os
 import statistics
 import sys
@@ -14,7 +14,8 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 cfg = bench.CONFIGS["rtow"]
 rt = bench.make_tracer(cfg, "f64", 1, 0)
 rt.render()
-for b in (0, 32, 0, 32):
+sizes = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 32]
+for b in sizes + sizes:
     ks, ws = [], []
     for _ in range(reps):
         t = time.perf_counter()

@@ -827,7 +827,10 @@ def test_progressive_preview_and_cancel(gpu):
     res = rt.render(want=("preview",), batch_samples=2, on_progress=lambda f: fr.append(f) and False)
     assert len(fr) >= 16 and all(x < y for x, y in zip(fr, fr[1:])) and fr[-1] == 1.0
     rt30 = _rtow(128, 72, 30, seed=6)
-    assert np.array_equal(res["preview"], rt30.render(batch_samples=2)["rgba8"])
+    # running frames come from preview_kernel, whose gamma pow is binary32 (pt_trace.hip): within one
+    # RGBA8 step of the exact frame, on pixels within ~1e-7 of a rounding boundary
+    d = np.abs(res["preview"].astype(np.int32) - rt30.render(batch_samples=2)["rgba8"].astype(np.int32))
+    assert d.max() <= 1 and np.count_nonzero(d) <= 1e-3 * d.size, (d.max(), np.count_nonzero(d))
     assert not np.array_equal(res["preview"], res["rgba8"])
     rt30.close()
     calls = []
@@ -866,14 +869,17 @@ np.savez(sys.argv[2], **out)
 
 
 def test_overlapped_batches_equal_serial_batches(gpu, tmp_path):
-    """Batches traced on two streams into their own chunk partials (the next batch's waves fill the CUs
-    while this one drains, reduces in batch order on the accumulation stream) give the same bits as the
+    """Batches traced in one fused launch (items batch-major, each batch reduced once its items are done)
+    and batches traced on three streams into their own chunk partials (RT_FUSED_BATCHES=0: the next
+    batch's waves fill the CUs while this one drains; reduces in batch order) give the same bits as the
     same batches run one after the other (forced here by a 1-MiB partials budget, too small for two
     slots): ragged last batches, a triangle BVH, and the whole-batch split over two devices (== the same
     batches one after the other on one device)."""
-    over = _render_in_child(_BATCH_SCRIPT, tmp_path / "over.npz")
+    over = _render_in_child(_BATCH_SCRIPT, tmp_path / "over.npz")                 # one device: fused batches
+    unfused = _render_in_child(_BATCH_SCRIPT, tmp_path / "unfused.npz", RT_FUSED_BATCHES="0")   # a launch per batch
     serial = _render_in_child(_BATCH_SCRIPT, tmp_path / "serial.npz", RT_PART_MB="1")
     two = "rtow.json.5.[0, 0]"          # the whole-batch split (two devices) == the same batches on one
     for k in over.files:
         ref = serial["rtow.json.5.None"] if k == two else serial[k]
         assert np.array_equal(over[k], ref, equal_nan=True), k
+        assert np.array_equal(unfused[k], ref, equal_nan=True), k
