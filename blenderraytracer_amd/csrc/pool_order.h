@@ -1,6 +1,7 @@
-// pool_order.h — the sample pool's 8x8 tiles and the order in which its (tile, chunk) items are
-// visited (pt_trace.hip).  Host-and-device code: tests/hostcheck enumerates the order on the CPU
-// (tests/test_pool_order.py checks that it is a permutation).
+// pool_order.h — the sample pool's 8x8 tiles, the order in which its (tile, chunk) items are visited
+// and the samples of each chunk (pt_trace.hip).  Host-and-device code: tests/hostcheck enumerates them
+// on the CPU (tests/test_pool_order.py: the order is a permutation; a fused launch's chunks are the
+// chunks of the per-batch launches).
 #pragma once
 #include "pt_path.h"
 
@@ -63,6 +64,18 @@ RT_HD unsigned item_at(const ImageParams& im, unsigned p, int tiles) {
     if constexpr (RT_TILE_BLOCK <= 1) return p;
     const unsigned ci = p / (unsigned)tiles;
     return ci * (unsigned)tiles + (unsigned)tile_at(im, (int)(p - ci * (unsigned)tiles));
+}
+
+// (batch, chunk within it, first sample, end sample) of launch chunk gci (ImageParams::batch_chunks)
+struct ChunkRange { int b, ci, sb, se; };
+RT_HD ChunkRange chunk_range(const ImageParams& im, int gci, int chunk) {
+    ChunkRange r;
+    r.b = im.batch_chunks ? gci / im.batch_chunks : 0;
+    r.ci = gci - r.b * im.batch_chunks;
+    const int bs = im.s_begin + r.b * im.batch_samples;
+    r.sb = bs + r.ci * chunk;
+    r.se = min(im.batch_chunks ? min(im.s_end, bs + im.batch_samples) : im.s_end, r.sb + chunk);
+    return r;
 }
 
 }  // namespace rt

@@ -132,18 +132,6 @@ __device__ __forceinline__ void mark_aborted(const Counters& c) {
     __hip_atomic_store(c.aborted, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// (batch, chunk within it, first sample, end sample) of launch chunk gci (ImageParams::batch_chunks)
-struct ChunkRange { int b, ci, sb, se; };
-__device__ __forceinline__ ChunkRange chunk_range(const ImageParams& im, int gci, int chunk) {
-    ChunkRange r;
-    r.b = im.batch_chunks ? gci / im.batch_chunks : 0;
-    r.ci = gci - r.b * im.batch_chunks;
-    const int bs = im.s_begin + r.b * im.batch_samples;
-    r.sb = bs + r.ci * chunk;
-    r.se = min(im.batch_chunks ? min(im.s_end, bs + im.batch_samples) : im.s_end, r.sb + chunk);
-    return r;
-}
-
 // A chunk partial of a fused launch: stored through to memory (sc1: agent-scope store), since the
 // reduce that reads it runs while this launch is still going, on whatever XCD
 __device__ __forceinline__ void store_through(double* p, double v) {

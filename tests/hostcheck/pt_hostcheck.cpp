@@ -365,3 +365,14 @@ extern "C" long long ptc_pool_order(int cw, int ch, int chunks, int one_wave, un
     params[2] = tiles;
     return n;
 }
+
+// chunk_range (pool_order.h, TEST TOOL): (batch, chunk, first sample, end sample) of launch chunk gci
+extern "C" void ptc_chunk_range(int s_begin, int s_end, int batch_samples, int batch_chunks, int gci, int chunk, int* out) {
+    ImageParams im{};
+    im.s_begin = s_begin;
+    im.s_end = s_end;
+    im.batch_samples = batch_samples;
+    im.batch_chunks = batch_chunks;
+    const ChunkRange r = chunk_range(im, gci, chunk);
+    out[0] = r.b; out[1] = r.ci; out[2] = r.sb; out[3] = r.se;
+}

@@ -54,3 +54,37 @@ def test_pool_order_odd_parameters(cw, ch, chunks):
         assert L.ptc_pool_order(cw, ch, chunks, one_wave, out.ctypes.data_as(C.POINTER(C.c_uint32)), par) == tiles * chunks
         assert (par[0], par[1], par[2]) == (3, 5, tiles)
         _check(out, tiles, chunks)
+
+
+def _chunk_range(L, s_begin, s_end, batch, batch_chunks, gci, chunk):
+    import ctypes as C
+    out = (C.c_int * 4)()
+    L.ptc_chunk_range(s_begin, s_end, batch, batch_chunks, gci, chunk, out)
+    return tuple(out)
+
+
+@pytest.mark.parametrize("s0,s1,batch,chunk", [(0, 512, 32, 32), (0, 24, 3, 3), (0, 17, 4, 4), (5, 17, 4, 3),
+                                               (0, 8, 2, 2), (0, 100, 7, 3), (3, 64, 16, 5), (0, 1000, 64, 45)])
+def test_fused_chunks_are_the_batches_chunks(s0, s1, batch, chunk):
+    """A fused launch (launch_trace_batches: every batch of a progressive render in one pool launch)
+    gives launch chunk gci the samples that chunk gci % batch_chunks of batch gci // batch_chunks has in
+    that batch's own launch, and an empty range to the chunks a short last batch does not have — so
+    the items, their partials and the reduces are those of one launch per batch (bit-identical sums;
+    the GPU test test_overlapped_batches_equal_serial_batches checks the images)."""
+    import ctypes as C
+    L = hc.lib()
+    L.ptc_chunk_range.argtypes = [C.c_int] * 6 + [C.POINTER(C.c_int)]
+    nb = -(-(s1 - s0) // batch)
+    chunks_b = -(-batch // chunk)
+    seen = []
+    for gci in range(nb * chunks_b):
+        b, ci, sb, se = _chunk_range(L, s0, s1, batch, chunks_b, gci, chunk)
+        assert (b, ci) == (gci // chunks_b, gci % chunks_b)
+        bb, be = s0 + b * batch, min(s1, s0 + (b + 1) * batch)      # batch b's own launch
+        nchunks = -(-(be - bb) // chunk)
+        if ci < nchunks:
+            assert (sb, se) == _chunk_range(L, bb, be, 0, 0, ci, chunk)[2:], (gci, b, ci)
+            seen.extend(range(sb, se))
+        else:
+            assert se <= sb, (gci, sb, se)                          # a short last batch's missing chunk
+    assert seen == list(range(s0, s1))                               # every sample once, in order
