@@ -234,10 +234,12 @@ void rt_scene_destroy(rt_scene* scene);
  * Replaces RayTracer.render (ray-tracer.js:166-281) minus the DOM. Synchronous.
  * progress(fraction, user) is called between sample batches from the calling thread; a non-zero
  * return value cancels (like window.renderCancelled, ray-tracer.js:190,196), as does rt_cancel from any
- * thread.  Batches are pipelined (up to 3 per device are queued on the GPU beyond the one the host waits
- * for).  With the sample pool and several batches a cancel stops every queued batch at its next 8x8
- * tile x sample-chunk item (about a millisecond on config 3) and the render returns once the GPU has
- * drained; the checkpoint holds the batches fully added before that.  Otherwise (sample order, one
+ * thread.  Batches are pipelined: on one device (up to 64 batches whose partials fit RT_FUSED_MB) all
+ * of them are traced by ONE launch and each batch is added as soon as its last item is done; otherwise
+ * up to 3 per device are queued on the GPU beyond the one the host waits for.  With the sample pool and
+ * several batches a cancel stops the batches within a few 8x8 tile x sample-chunk items (the LDS pool
+ * kernel checks every 4th item of each wave: a few milliseconds on config 3) and the render returns
+ * once the GPU has drained; the checkpoint holds the batches fully added before that.  Otherwise (sample order, one
  * batch, partials that do not fit) it is observed between batches and the queued ones complete.
  * RT_ERR_CANCELLED unless every sample was traced.
  * Threading: one call in flight per scene (rt_render, rt_render_resume, rt_trace_device,
@@ -289,7 +291,7 @@ int rt_closest_hits(rt_scene* scene, int32_t precision, int32_t accel, const dou
  * walk finds the same closest hit; they differ in speed only. */
 int rt_scene_walk(rt_scene* scene, int32_t precision, int32_t accel);
 
-/* Request cancellation of an in-flight rt_render on `scene` (the pool kernels read it before every item;
+/* Request cancellation of an in-flight rt_render on `scene` (the pool kernels read it between items;
  * see rt_render). */
 int rt_cancel(rt_scene* scene);
 
