@@ -392,8 +392,30 @@ RT_HD bool better(R t, int obj, int id, const Closest<R>& b) {
 // = hb, so sqrt(disc) <= hb, both roots are <= 0 < tmin, and the reference's test rejects as well (NaN
 // operands fail the comparisons and take the full test).  Used for the dominant spheres, which every
 // ray leaving them (the RTOW ground: most secondary rays) would otherwise test in full: +0.9 %.
+// RT_ROOT_RCP: the roots' divisions by a = d.d as Markstein corrections from ya = RN(1/a), computed
+// once per closest-hit query (the grid walk; ya = 0: the plain divisions), guarded so that every
+// intermediate is normal: 2^-500 <= |-hb -+ sqrt(disc)| <= 2^500 (the caller: 2^-400 <= a <= 2^400)
+#ifndef RT_ROOT_RCP
+#define RT_ROOT_RCP 0             // A/B pending
+#endif
+template <class R> RT_HD R root_div(R x, R a, R ya) {
+    const R ax = fabs(x);
+    if (RT_ROOT_RCP && ya != (R)0 && ax >= (R)(sizeof(R) == 8 ? 0x1p-500 : 0x1p-60) &&
+        ax <= (R)(sizeof(R) == 8 ? 0x1p500 : 0x1p60)) {
+        const R q0 = x * ya;
+        return fma(fma(-q0, a, x), ya, q0);
+    }
+    return x / a;
+}
+// RN(1/a) for root_div when a lies in its range, else 0
+template <class R> RT_HD R root_rcp(R a) {
+    const bool in = a >= (R)(sizeof(R) == 8 ? 0x1p-400 : 0x1p-40) && a <= (R)(sizeof(R) == 8 ? 0x1p400 : 0x1p40);
+    return RT_ROOT_RCP && in ? (R)1 / a : (R)0;
+}
+
 template <class R>
-RT_HD bool sphere_candidate(const SphereRec<R>& s, V3<R> o, V3<R> d, R a, R tmin, R& t, bool away = false) {   // geometry.js:15-45
+RT_HD bool sphere_candidate(const SphereRec<R>& s, V3<R> o, V3<R> d, R a, R tmin, R& t, bool away = false,
+                            R ya = (R)0) {   // geometry.js:15-45
     RT_HCOUNT(HC_F64_TESTS, 1);
     R ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
     R hb = ocx * d.x + ocy * d.y + ocz * d.z;
@@ -403,10 +425,10 @@ RT_HD bool sphere_candidate(const SphereRec<R>& s, V3<R> o, V3<R> d, R a, R tmin
     if (disc < (R)0) return false;
     RT_HCOUNT(HC_DISC_OK, 1);
     R sq = sqrt(disc);
-    t = (-hb - sq) / a;
+    t = root_div(-hb - sq, a, ya);
     if (!(t < tmin)) return true;
     RT_HCOUNT(HC_SECOND_ROOT, 1);
-    t = (-hb + sq) / a;
+    t = root_div(-hb + sq, a, ya);
     return !(t < tmin);
 }
 
@@ -678,14 +700,14 @@ RT_HD void brute_planes_boxes(const SceneView<R>& sc, V3<R> o, V3<R> d, R tmin, 
 // Sphere records [first, end) of `recs` (a BVH leaf, or the dominant spheres) against the current best.
 template <class R>
 RT_HD void sphere_records(const SphereLeaf<R>* recs, int first, int end, V3<R> o, V3<R> d, R a, const FilterRay& fr,
-                          R tmin, Closest<R>& b, float& tl, Work& w, bool away = false) {
+                          R tmin, Closest<R>& b, float& tl, Work& w, bool away = false, R ya = (R)0) {
     RT_COUNT(w.spheres += end - first);
     for (int k = first; k < end; ++k) {
         const SphereLeaf<R> L = recs[k];
         if constexpr (sizeof(R) == 8)
             if (!sphere_filter_pass(L.f, fr)) continue;
         R t;
-        if (!sphere_candidate(L.s, o, d, a, tmin, t, away)) continue;
+        if (!sphere_candidate(L.s, o, d, a, tmin, t, away, ya)) continue;
         if (better(t, L.obj, L.id, b)) {
             b = Closest<R>{t, HIT_SPHERE, L.id, L.mat, L.obj};
             tl = bvh_tlimit(b.t);
@@ -779,7 +801,7 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
 #endif
 template <class R>
 RT_HD void sphere_records_lds(const rt_u4* lrec, const SphereLeaf<R>* recs, int first, int end, V3<R> o, V3<R> d,
-                              R a, const FilterRay& fr, R tmin, Closest<R>& b, float& tl, Work& w) {
+                              R a, const FilterRay& fr, R tmin, Closest<R>& b, float& tl, Work& w, R ya = (R)0) {
     RT_COUNT(w.spheres += end - first);
     if constexpr (sizeof(R) == 8 && RT_GRID_COMPACT != 0) {
         for (int base = first; base < end; base += 32) {
@@ -797,7 +819,7 @@ RT_HD void sphere_records_lds(const rt_u4* lrec, const SphereLeaf<R>* recs, int 
                 const SphereRec<R> s = recs[k].s;
                 const int id = recs[k].id, obj = recs[k].obj, mat = recs[k].mat;
                 R t;
-                if (!sphere_candidate(s, o, d, a, tmin, t)) continue;
+                if (!sphere_candidate(s, o, d, a, tmin, t, false, ya)) continue;
                 if (better(t, obj, id, b)) {
                     b = Closest<R>{t, HIT_SPHERE, id, mat, obj};
                     tl = bvh_tlimit(b.t);
@@ -822,7 +844,7 @@ RT_HD void sphere_records_lds(const rt_u4* lrec, const SphereLeaf<R>* recs, int 
             id = (int)q1.x; obj = (int)q1.y; mat = (int)q1.z;
         }
         R t;
-        if (!sphere_candidate(s, o, d, a, tmin, t)) continue;
+        if (!sphere_candidate(s, o, d, a, tmin, t, false, ya)) continue;
         if (better(t, obj, id, b)) {
             b = Closest<R>{t, HIT_SPHERE, id, mat, obj};
             tl = bvh_tlimit(b.t);
@@ -855,10 +877,10 @@ RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
     brute_planes_boxes(sc, o, d, tmin, b);
     float tl = bvh_tlimit(b.t);
-    const R a = dot(d, d);
+    const R a = dot(d, d), ya = root_rcp(a);
     FilterRay fr{};
     if constexpr (sizeof(R) == 8) fr = make_filter_ray(o, d);
-    if (sc.num_big_spheres > 0) sphere_records(sc.big_spheres, 0, sc.num_big_spheres, o, d, a, fr, tmin, b, tl, w, true);
+    if (sc.num_big_spheres > 0) sphere_records(sc.big_spheres, 0, sc.num_big_spheres, o, d, a, fr, tmin, b, tl, w, true, ya);
     if (sc.num_grid_cells <= 0) return b;
     const float of[3] = {(float)o.x, (float)o.y, (float)o.z};
     const float df[3] = {(float)d.x, (float)d.y, (float)d.z};
@@ -898,7 +920,7 @@ RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work
         RT_COUNT(++w.nodes);
         const int ci = cell[0] + sc.grid_n[0] * (cell[1] + sc.grid_n[1] * cell[2]);
         if constexpr (LDSG) {
-            sphere_records_lds(stk.grec, sc.grid_leaf, stk.gcell[ci], stk.gcell[ci + 1], o, d, a, fr, tmin, b, tl, w);
+            sphere_records_lds(stk.grec, sc.grid_leaf, stk.gcell[ci], stk.gcell[ci + 1], o, d, a, fr, tmin, b, tl, w, ya);
         } else {
 #if RT_GRID_UNIFORM && defined(__HIP_DEVICE_COMPILE__)
         // every active lane in one cell: its range and records through scalar loads

@@ -376,3 +376,8 @@ extern "C" void ptc_chunk_range(int s_begin, int s_end, int batch_samples, int b
     const ChunkRange r = chunk_range(im, gci, chunk);
     out[0] = r.b; out[1] = r.ci; out[2] = r.sb; out[3] = r.se;
 }
+
+// root_div (pt_core.h RT_ROOT_RCP, TEST TOOL): x / a through RN(1 / a) and a Markstein correction
+extern "C" void ptc_root_div(const double* x, const double* a, double* out, long long n) {
+    for (long long i = 0; i < n; ++i) out[i] = rt::root_div<double>(x[i], a[i], rt::root_rcp<double>(a[i]));
+}
