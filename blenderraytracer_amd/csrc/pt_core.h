@@ -394,13 +394,16 @@ RT_HD bool better(R t, int obj, int id, const Closest<R>& b) {
 // ray leaving them (the RTOW ground: most secondary rays) would otherwise test in full: +0.9 %.
 // RT_ROOT_RCP: the roots' divisions by a = d.d as Markstein corrections from ya = RN(1/a), computed
 // once per closest-hit query (the grid walk; ya = 0: the plain divisions), guarded so that every
-// intermediate is normal: 2^-500 <= |-hb -+ sqrt(disc)| <= 2^500 (the caller: 2^-400 <= a <= 2^400)
+// intermediate is normal: 2^-500 <= |-hb -+ sqrt(disc)| <= 2^500 (the caller: 2^-400 <= a <= 2^400;
+// binary32: 2^-60, 2^60, 2^-40, 2^40).  0: never / 1: both precisions / 2: binary32 only (RTOW 256
+// spp: f32 +2.0 %, f64 ±0 — DESIGN.md §4; bit-identical images either way)
 #ifndef RT_ROOT_RCP
-#define RT_ROOT_RCP 0             // A/B pending
+#define RT_ROOT_RCP 2
 #endif
+template <class R> constexpr bool root_rcp_on() { return RT_ROOT_RCP == 1 || (RT_ROOT_RCP == 2 && sizeof(R) == 4); }
 template <class R> RT_HD R root_div(R x, R a, R ya) {
     const R ax = fabs(x);
-    if (RT_ROOT_RCP && ya != (R)0 && ax >= (R)(sizeof(R) == 8 ? 0x1p-500 : 0x1p-60) &&
+    if (root_rcp_on<R>() && ya != (R)0 && ax >= (R)(sizeof(R) == 8 ? 0x1p-500 : 0x1p-60) &&
         ax <= (R)(sizeof(R) == 8 ? 0x1p500 : 0x1p60)) {
         const R q0 = x * ya;
         return fma(fma(-q0, a, x), ya, q0);
@@ -410,7 +413,7 @@ template <class R> RT_HD R root_div(R x, R a, R ya) {
 // RN(1/a) for root_div when a lies in its range, else 0
 template <class R> RT_HD R root_rcp(R a) {
     const bool in = a >= (R)(sizeof(R) == 8 ? 0x1p-400 : 0x1p-40) && a <= (R)(sizeof(R) == 8 ? 0x1p400 : 0x1p40);
-    return RT_ROOT_RCP && in ? (R)1 / a : (R)0;
+    return root_rcp_on<R>() && in ? (R)1 / a : (R)0;
 }
 
 template <class R>

@@ -381,3 +381,6 @@ extern "C" void ptc_chunk_range(int s_begin, int s_end, int batch_samples, int b
 extern "C" void ptc_root_div(const double* x, const double* a, double* out, long long n) {
     for (long long i = 0; i < n; ++i) out[i] = rt::root_div<double>(x[i], a[i], rt::root_rcp<double>(a[i]));
 }
+extern "C" void ptc_root_div_f32(const float* x, const float* a, float* out, long long n) {
+    for (long long i = 0; i < n; ++i) out[i] = rt::root_div<float>(x[i], a[i], rt::root_rcp<float>(a[i]));
+}

@@ -8,14 +8,15 @@ import numpy as np
 from tests import hostcheck_binding as hc
 
 
-def _root_div(x, a):
-    L = hc.lib(("RT_ROOT_RCP=1",))            # the Markstein path, whatever the build's default
-    L.ptc_root_div.argtypes = [C.POINTER(C.c_double)] * 3 + [C.c_longlong]
-    x = np.ascontiguousarray(x, dtype=np.float64)
-    a = np.ascontiguousarray(a, dtype=np.float64)
+def _root_div(x, a, dtype=np.float64):
+    L = hc.lib(("RT_ROOT_RCP=1",))            # the Markstein path in both precisions, whatever the default
+    fn, ct = (L.ptc_root_div, C.c_double) if dtype == np.float64 else (L.ptc_root_div_f32, C.c_float)
+    fn.argtypes = [C.POINTER(ct)] * 3 + [C.c_longlong]
+    x = np.ascontiguousarray(x, dtype=dtype)
+    a = np.ascontiguousarray(a, dtype=dtype)
     out = np.empty_like(x)
-    p = lambda v: v.ctypes.data_as(C.POINTER(C.c_double))   # noqa: E731
-    L.ptc_root_div(p(x), p(a), p(out), len(x))
+    p = lambda v: v.ctypes.data_as(C.POINTER(ct))   # noqa: E731
+    fn(p(x), p(a), p(out), len(x))
     return out
 
 
@@ -43,3 +44,15 @@ def test_root_div_edges():
     got = _root_div(x, a)
     assert np.array_equal(np.isnan(got), np.isnan(ref))
     assert np.array_equal(got[~np.isnan(ref)].view(np.uint64), ref[~np.isnan(ref)].view(np.uint64))
+
+
+def test_root_div_equals_division_binary32():
+    """The binary32 fast mode's form (RT_ROOT_RCP's default): the same Markstein correction in binary32."""
+    rng = np.random.default_rng(11)
+    n = 2_000_000
+    a = np.concatenate([rng.uniform(0.25, 4.0, n // 2), np.exp2(rng.uniform(-45, 45, n // 2))]).astype(np.float32)
+    x = np.concatenate([rng.normal(0, 10, n // 2), np.exp2(rng.uniform(-65, 65, n // 2)) * rng.choice([-1, 1], n // 2)]).astype(np.float32)
+    with np.errstate(all="ignore"):
+        ref = x / a
+    got = _root_div(x, a, np.float32)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), int(np.count_nonzero(got != ref))
