@@ -864,11 +864,20 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     // samples, chunk being the pool's rule for the whole render (as one device's batches do), so the
     // sums are bit-identical to the same batches on one device.
     bool whole = nsh > 1 && pool && s->max_depth > 0 && overlap_env && s1 > s0;
+    // A batch of B samples is split into round(B / h) equal chunks (at least one), h being the pool's
+    // rule for the render's whole share: min(h, B)-sample chunks left a short remainder chunk in every
+    // batch (mesh50k in 16 batches of 16 spp: chunks of 12 + 4, 77.2 ms vs 75.0 ms as one 16-sample
+    // chunk).  B is the batch setting, not the samples left, so a resume sees the same chunks.
+    auto balanced = [](int h, int b) {
+        if (h <= 0 || b <= 0) return h;
+        const int n = std::max(1, (int)std::lround((double)b / (double)h));
+        return (b + n - 1) / n;
+    };
     int whole_batch = 0, whole_chunk = 0;
     if (whole) {
         const int full = s->batch_samples > 0 ? s->batch_samples : std::max(1, s1 - base);
         whole_batch = std::max(1, std::min(full, (s1 - base + nsh - 1) / nsh));
-        whole_chunk = pool_plan(cw, ch, std::max(1, s1 - base), sc->tri_bvh).chunk;
+        whole_chunk = balanced(pool_plan(cw, ch, std::max(1, s1 - base), sc->tri_bvh).chunk, whole_batch);
         const int ns = std::min(whole_batch, s1 - s0);
         const size_t bytes = pool_plan(cw, ch, ns, sc->tri_bvh, std::min(whole_chunk, ns)).part_bytes;
         for (int k = 0; k < nsh && whole; ++k) {    // every device's partial slots must fit, else split batches
@@ -882,14 +891,16 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     std::vector<Counters> cs(nsh);
     // Several batches (split mode): every batch's pool waves take min(batch, chunk) samples, chunk being
     // the pool's rule for the shard's whole share of the render (not for one batch: short chunks lengthen
-    // each wave's drain relative to its work).  The same batches give the same chunks on a resume (the
-    // share is counted from sample_begin), so a resumed render stays bit-identical.
+    // each wave's drain relative to its work), balanced over the shard's part of a full batch.  The same
+    // batches give the same chunks on a resume (the share is counted from sample_begin), so a resumed
+    // render stays bit-identical.
     std::vector<int> chunk_hint(nsh, whole ? whole_chunk : 0);
     if (pool && nb > 1 && !whole)
         for (int k = 0; k < nsh; ++k) {
-            int a, b;
+            int a, b, fa, fb;
             shard_range(base, s1, k, nsh, a, b);
-            chunk_hint[k] = pool_plan(cw, ch, std::max(1, b - a), sc->tri_bvh).chunk;
+            shard_range(0, batch, k, nsh, fa, fb);
+            chunk_hint[k] = balanced(pool_plan(cw, ch, std::max(1, b - a), sc->tri_bvh).chunk, fb - fa);
         }
     auto batch_chunk = [&](int k, int ns) { return chunk_hint[k] > 0 ? std::max(1, std::min(chunk_hint[k], ns)) : 0; };
     // overlapped batches: the pool with several batches (always in whole-batch mode).  Not with per-pixel

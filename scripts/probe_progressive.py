@@ -1,6 +1,6 @@
 """Progressive-render cost probe (DEV TOOL): config 3 as one batch and as 16 batches of 32 spp, each
 rendered `reps` times; prints the median kernel and wall time.
-usage: python scripts/probe_progressive.py [reps] [batch sizes, comma-separated; 0 = one batch]"""
+usage: [PROBE_CONFIG=mesh50k] python scripts/probe_progressive.py [reps] [batch sizes, comma-separated; 0 = one batch]"""
 import os
 import statistics
 import sys
@@ -11,7 +11,7 @@ import torch  # noqa: F401,E402
 import bench  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-cfg = bench.CONFIGS["rtow"]
+cfg = bench.CONFIGS[os.environ.get("PROBE_CONFIG", "rtow")]
 rt = bench.make_tracer(cfg, "f64", 1, 0)
 rt.render()
 sizes = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 32]
