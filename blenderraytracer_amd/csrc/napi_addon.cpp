@@ -6,6 +6,7 @@
 //   render(scene, settings, progress?) -> Promise<{mean?, post?, rgba8, segments?, draws?, stats}>
 //                                         (rt_render on a libuv worker thread: the event loop stays live)
 //   cancel(scene)                      -> rt_cancel (the queued batches stop at their next item)
+//   checkpoint(scene) -> {sums, samplesDone}; checkpointSamples(scene) -> samplesDone (sums stay resident)
 //   destroyScene(scene), deviceCount(), abiVersion()
 // Progress reaches JS through a napi_threadsafe_function, in order and before the Promise settles (the
 // worker waits until the main thread has run each call, as the reference calls onProgress inside its
@@ -229,6 +230,7 @@ struct RenderJob {
     std::atomic<int> cancel_from_js{0};
     std::vector<double> resume;     // settings.resumeSums (rt_render_resume)
     int32_t resume_done = -1;
+    bool resume_resident = false;   // settings.resumeResident: the scene's own checkpoint (sums NULL)
 };
 
 // The caller's typed array behind `ref` if it is still attached and holds `bytes` bytes, else nullptr.
@@ -299,8 +301,8 @@ void execute(napi_env, void* data) {
     const double t0 = trace_ms();
     if (t0 >= 0) fprintf(stderr, "[napi] rt_render start %.3f ms\n", t0);
     if (job->resume_done >= 0)
-        job->status = rt_render_resume(job->scene, &job->st, job->resume.data(), job->resume_done, &out, progress_hook,
-                                       job, &job->stats);
+        job->status = rt_render_resume(job->scene, &job->st, job->resume_resident ? nullptr : job->resume.data(),
+                                       job->resume_done, &out, progress_hook, job, &job->stats);
     else
         job->status = rt_render(job->scene, &job->st, &out, progress_hook, job, &job->stats);
     if (job->status != RT_OK) job->error = rt_last_error();
@@ -449,6 +451,9 @@ napi_value render(napi_env env, napi_callback_info info) {
         }
         job->resume.assign(static_cast<double*>(rs), static_cast<double*>(rs) + job->n * 3);
         job->resume_done = (int32_t)get_num(env, s, "resumeSamplesDone", 0);
+    } else if (get_num(env, s, "resumeResident", 0) != 0) {      // continue from the checkpoint on the device
+        job->resume_resident = true;
+        job->resume_done = (int32_t)get_num(env, s, "resumeSamplesDone", 0);
     }
     st.sum_order = (int32_t)get_num(env, s, "sumOrder", RT_SUM_POOL);
     // output buffers (see RenderJob): post unless settings.wantPost is 0; the RGBA8 frame also goes into
@@ -534,6 +539,23 @@ napi_value checkpoint(napi_env env, napi_callback_info info) {
     return res;
 }
 
+// checkpointSamples(scene) -> samplesDone of the scene's checkpoint, without copying its sums (they stay
+// on the device until the scene's next render: render(scene, {..., resumeResident: 1, resumeSamplesDone})
+// continues from them, checkpoint(scene) copies them out)
+napi_value checkpoint_samples(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_OK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    SceneBox* box = argc ? get_box(env, argv[0]) : nullptr;
+    if (!box || !box->sc) return throw_err(env, "checkpointSamples(scene)");
+    if (box->busy) return throw_err(env, "checkpointSamples: a render is in flight");
+    int32_t done = 0;
+    if (rt_render_checkpoint(box->sc, nullptr, 0, &done) != RT_OK) return throw_err(env, rt_last_error());
+    napi_value d;
+    NAPI_OK(napi_create_int32(env, done, &d));
+    return d;
+}
+
 napi_value destroy_scene(napi_env env, napi_callback_info info) {
     size_t argc = 1;
     napi_value argv[1];
@@ -566,6 +588,7 @@ napi_value init(napi_env env, napi_value exports) {
         {"render", nullptr, render, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"cancel", nullptr, cancel, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"checkpoint", nullptr, checkpoint, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"checkpointSamples", nullptr, checkpoint_samples, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"destroyScene", nullptr, destroy_scene, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"deviceCount", nullptr, device_count, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"abiVersion", nullptr, abi_version, nullptr, nullptr, nullptr, napi_enumerable, nullptr},

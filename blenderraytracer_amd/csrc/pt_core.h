@@ -39,7 +39,7 @@ extern unsigned long long rt_host_count[16];
 #endif
 enum HostCount { HC_F64_TESTS = 0, HC_DISC_OK, HC_SECOND_ROOT, HC_ACCEPT, HC_LAMBERT, HC_METAL, HC_DIELECTRIC,
                  HC_EMISSIVE, HC_MISS, HC_SAMPLES, HC_SPHERE_DRAW_ROUNDS, HC_DISK_DRAW_ROUNDS, HC_FILTER_TESTS,
-                 HC_DIELECTRIC_SCHLICK };
+                 HC_DIELECTRIC_SCHLICK, HC_TRI_FILTERS, HC_TRI_TESTS };
 
 // ---- keyed RNG ------------------------------------------------------------------
 RT_HD uint32_t lowbias32(uint32_t x) {
@@ -79,24 +79,45 @@ template <class R> RT_HD R dot(V3<R> a, V3<R> b) { return a.x * b.x + a.y * b.y 
 template <class R> RT_HD V3<R> cross(V3<R> a, V3<R> b) {
     return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
-// RT_DIV_RCP: a vector divided by one scalar s as three Markstein corrections from y = RN(1/s)
-// instead of three IEEE divisions: q0 = RN(x y), e = x - q0 s exactly (FMA), RN(q0 + e y) = RN(x / s)
-// when nothing under- or overflows (Markstein's theorem; 2e8 random binary64 pairs bit-identical to the
-// division on the host).  Guarded: outside 2^-900 <= |x|, 2^-400 <= |s| <= 2^400 (binary32: 2^-100,
-// 2^-40 .. 2^40) — zero components included — the plain divisions run.  The sphere normal's (p - c) / r
-// uses RN(1/r) precomputed per sphere (no division left), normalize one division for y: RTOW f64 +0.9 %,
-// f32 +1.2 % (round 1's form, with a runtime reciprocal and refinement, measured -3.5 %).
+// RT_DIV_RCP: a vector divided by one scalar s through y = RN(1/s) instead of three IEEE divisions.
+// Markstein's theorem: if q is a faithful rounding of x/s (within 1 ulp) and y = RN(1/s), then with the
+// exact remainder e = x - q s (one FMA) RN(q + e y) = RN(x / s), when nothing under- or overflows.
+// q0 = RN(x y) is NOT always faithful (it can be 1.5 ulp off: y's error times x, plus q0's rounding), so
+// binary64 — the reference's arithmetic — takes one correction more: q1 = RN(q0 + RN(x - q0 s) y) is within
+// 1/2 ulp + 2^-100 ulp of x/s, hence faithful, and the second correction RN(q1 + (x - q1 s) y) is the
+// correctly rounded quotient by the theorem (5 binary64 ops instead of a ~22-slot division).  Binary32
+// (the non-conforming fast mode) keeps the single correction, bit-identical to the division on every
+// significand of x for 2,000+ divisors (tests/test_root_div.py).  Guarded so that every intermediate is a
+// normal number: 2^-500 <= |x| <= 2^500 and 2^-400 <= |s| <= 2^400, so |x / s| lies in [2^-900, 2^900]
+// (binary32: 2^-60 .. 2^60, 2^-40 .. 2^40); outside — zero components included — the plain divisions run.
+// The sphere normal's (p - c) / r uses RN(1/r) precomputed per sphere (no division left), normalize one
+// division for y.  Single correction in both precisions: RTOW f64 +0.9 %, f32 +1.2 % (DESIGN.md §4;
+// round 1's form, a runtime reciprocal and refinement, measured -3.5 %).
 #ifndef RT_DIV_RCP
 #define RT_DIV_RCP 1
 #endif
+#ifndef RT_DIV_F64_TWICE
+#define RT_DIV_F64_TWICE 1        // 0 (A/B): round 4's single correction in binary64 too
+#endif
+#ifndef RT_DIV_RCP_F64
+#define RT_DIV_RCP_F64 1          // 0 (A/B): binary64 vectors through the IEEE divisions
+#endif
+template <class R> constexpr bool div_rcp_on() { return RT_DIV_RCP && (sizeof(R) == 4 || RT_DIV_RCP_F64); }
+template <class R> RT_HD R div_rcp_1(R x, R s, R y) {           // guarded by the caller
+    const R q0 = x * y;
+    const R q1 = fma(fma(-q0, s, x), y, q0);
+    if constexpr (sizeof(R) == 4 || RT_DIV_F64_TWICE == 0) return q1;
+    return fma(fma(-q1, s, x), y, q1);
+}
+template <class R> RT_HD bool div_rcp_range(R x) {
+    const R ax = fabs(x);
+    return ax >= (R)(sizeof(R) == 8 ? 0x1p-500 : 0x1p-60) && ax <= (R)(sizeof(R) == 8 ? 0x1p500 : 0x1p60);
+}
 template <class R> RT_HD V3<R> vdiv_rcp(V3<R> a, R s, R y) {
-    const R xmin = sizeof(R) == 8 ? (R)0x1p-900 : (R)0x1p-100;
     const R smin = sizeof(R) == 8 ? (R)0x1p-400 : (R)0x1p-40, smax = sizeof(R) == 8 ? (R)0x1p400 : (R)0x1p40;
     const R as = fabs(s);
-    if (fabs(a.x) >= xmin && fabs(a.y) >= xmin && fabs(a.z) >= xmin && as >= smin && as <= smax) {
-        auto q = [&](R x) { const R q0 = x * y; return fma(fma(-q0, s, x), y, q0); };
-        return {q(a.x), q(a.y), q(a.z)};
-    }
+    if (div_rcp_on<R>() && div_rcp_range(a.x) && div_rcp_range(a.y) && div_rcp_range(a.z) && as >= smin && as <= smax)
+        return {div_rcp_1(a.x, s, y), div_rcp_1(a.y, s, y), div_rcp_1(a.z, s, y)};
     return vdiv(a, s);
 }
 template <class R> RT_HD V3<R> normalize(V3<R> a) {          // math.js:18
@@ -136,6 +157,10 @@ template <class R> struct TriGeom { R v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2
 // (the material is read from SceneView::tri_mat when a triangle is accepted: 80 / 48 B instead of 96 / 64,
 // mesh50k f32 +1.6 %, f64 ±0)
 template <class R> struct alignas(16) TriLeaf { TriGeom<R> t; int id, obj; };                           // 80 / 48 B
+// binary32 pre-filter record of a triangle (binary64 mode only; leaf order, beside TriLeaf<double>):
+// v0, e1, e2 rounded to binary32 and n = e2 x e1 (computed in binary64, rounded); n is NaN for a triangle
+// outside the filter's range (tri_filter_bound: then it is never rejected).  48 B
+struct alignas(16) TriFilter { float v0[3], e1[3], e2[3], n[3]; };
 
 // BVH node (32 B), nodes in depth-first preorder: an internal node's first child is the next node,
 // `skip` is the index just past its subtree.  fc = (first << 4) | count for a leaf of `count` <= 15
@@ -181,6 +206,7 @@ struct SceneView {
     const BvhNode* tri_nodes;
     int num_tri_nodes;
     const TriLeaf<R>* bvh_tri_leaf;
+    const TriFilter* tri_filter;   // binary64: the triangle leaves' binary32 pre-filter records (same order)
     const Bvh2Node* sphere_wide;   // two-child nodes of the two trees (preorder)
     const Bvh2Node* tri_wide;
     int num_sphere_wide, num_tri_wide;
@@ -402,12 +428,8 @@ RT_HD bool better(R t, int obj, int id, const Closest<R>& b) {
 #endif
 template <class R> constexpr bool root_rcp_on() { return RT_ROOT_RCP == 1 || (RT_ROOT_RCP == 2 && sizeof(R) == 4); }
 template <class R> RT_HD R root_div(R x, R a, R ya) {
-    const R ax = fabs(x);
-    if (root_rcp_on<R>() && ya != (R)0 && ax >= (R)(sizeof(R) == 8 ? 0x1p-500 : 0x1p-60) &&
-        ax <= (R)(sizeof(R) == 8 ? 0x1p500 : 0x1p60)) {
-        const R q0 = x * ya;
-        return fma(fma(-q0, a, x), ya, q0);
-    }
+    // the same guarded corrections as vdiv_rcp (two in binary64, one in binary32)
+    if (root_rcp_on<R>() && ya != (R)0 && div_rcp_range(x)) return div_rcp_1(x, a, ya);
     return x / a;
 }
 // RN(1/a) for root_div when a lies in its range, else 0
@@ -449,6 +471,81 @@ RT_HD bool triangle_candidate(const Tri& tr, V3<R> o, V3<R> d, R tmin, R& t) {  
     if (v < (R)0 || u + v > (R)1) return false;
     t = f * (tr.e2x * qx + tr.e2y * qy + tr.e2z * qz);
     return !(t < tmin);
+}
+
+// tri_filter_bound.  The binary64 test above decides through four quantities of exact inputs o, d, v0, e1,
+// e2: A = e1.(d x e2) (|A| < 1e-4 rejects), X = S.(d x e2) (u = X / A), Y = d.(S x e1) (v = Y / A) and
+// Z = e2.(S x e1) (t = Z / A), S = o - v0.  With C = d x S and n = e2 x e1 these are A = d.n, X = -e2.C,
+// Y = e1.C, Z = -S.n: the binary32 filter evaluates those forms (21 FMA-chained ops) from o, d, v0, e1,
+// e2 rounded to binary32 and n rounded from its binary64 value.  With u = 2^-24, md = |d|inf, me1 = |e1|inf,
+// me2 = |e2|inf and Ms = |o|inf + |v0|inf, the rounding of every input and operation bounds the errors
+// (components: |d_j S_k - d32_j S32_k| <= 3.02u md Ms, |C32_i - C_i| <= 9.1u md Ms, |n32_i - n_i| <= 2.01u
+// me1 me2, three-term dot products adding u (2 + 4 + 6) of their magnitude) by
+//   |A32 - A| <= 25u md me1 me2,  |X32 - X| <= 46u md me2 Ms,  |Y32 - Y| <= 46u md me1 Ms,
+//   |Z32 - Z| <= 31u me1 me2 Ms,
+// and the binary64 test's own values (X64 ...) lie within 46 * 2^-53 of the same magnitudes of the exact
+// ones.  The filter uses E = K P with K = 80u (1.7x margin, which also covers the binary32 evaluation of
+// the bounds), P the magnitude product above; Ms carries +2^-30, so no E is subnormal.  Given |A32| > Ea
+// (so sign(A64) = sign(A32) = s and A64 != 0), it rejects only what the binary64 test rejects:
+//   R0  |A32| + Ea < 0.99999e-4            -> |A64| < 1e-4
+//   R1  s X32 < -EX                         -> u64 = RN(RN(1/A64) X64) < 0 (nonzero: |X64| >= 0.4 EX)
+//   R2  s Y32 < -EY                         -> v64 < 0
+//   R4  W = s X32 + s Y32 - |A32| > EX + EY + Ea + 2^-22 (|W| + |A32|)
+//                                           -> X / A + Y / A >= 1 + 2^-40, so u64 > 1, v64 < 0 or u64 + v64 > 1
+//   R5  G = s Z32 - T |A32|, G + 2^-22 |G| + EZ + T Ea < 0 (T = 0.00099999)
+//                                           -> Z / A < T, so t64 < 0.001
+//   R6  G = s Z32 - tl |A32|, G - 2^-22 |G| - EZ - tl Ea > 0 (tl = bvh_tlimit(best) >= best (1 + 2^-21))
+//                                           -> t64 > best: `better` fails
+// (u > 1 alone needs no test of its own: with v >= 0 it implies R4's condition, with v < 0 R2's.)  Every
+// test is a comparison that fails on NaN, so NaN inputs, rays with |d|inf outside [2^-30, 2^30] or |o|inf
+// above 2^30 (md = NaN) and triangles outside the same range (n = NaN, scene_pack.h) are never rejected.
+// tests/test_tri_filter.py checks this on adversarial rays through edges, vertices and grazing planes.
+struct TriRay { float o[3], d[3], mo, md, mdK; };
+
+template <class R>
+RT_HD TriRay make_tri_ray(V3<R> o, V3<R> d) {
+    TriRay r;
+    r.o[0] = (float)o.x; r.o[1] = (float)o.y; r.o[2] = (float)o.z;
+    r.d[0] = (float)d.x; r.d[1] = (float)d.y; r.d[2] = (float)d.z;
+    // bounds on the binary64 values' magnitudes (rounded up), plus the 2^-30 floor of Ms
+    const float mo = fmaxf(fabsf(r.o[0]), fmaxf(fabsf(r.o[1]), fabsf(r.o[2]))) * (1.0f + 0x1p-22f);
+    const float md = fmaxf(fabsf(r.d[0]), fmaxf(fabsf(r.d[1]), fabsf(r.d[2]))) * (1.0f + 0x1p-22f);
+    const bool ok = mo <= 0x1p30f && md >= 0x1p-30f && md <= 0x1p30f;
+    r.mo = mo + 0x1p-30f;
+    r.md = ok ? md : NAN;
+    r.mdK = r.md * 0x5p-20f;                 // K = 80u = 5 * 2^-20
+    return r;
+}
+
+// false only if the binary64 test (triangle_candidate + `better` against a best whose limit is tl) certainly
+// rejects the triangle: tri_filter_bound above
+RT_HD bool tri_filter_pass(const TriFilter& f, const TriRay& r, float tl) {
+    RT_HCOUNT(HC_TRI_FILTERS, 1);
+    const float sx = r.o[0] - f.v0[0], sy = r.o[1] - f.v0[1], sz = r.o[2] - f.v0[2];
+    const float cx = __builtin_fmaf(r.d[1], sz, -(r.d[2] * sy));
+    const float cy = __builtin_fmaf(r.d[2], sx, -(r.d[0] * sz));
+    const float cz = __builtin_fmaf(r.d[0], sy, -(r.d[1] * sx));
+    const float A = __builtin_fmaf(r.d[0], f.n[0], __builtin_fmaf(r.d[1], f.n[1], r.d[2] * f.n[2]));
+    const float X = __builtin_fmaf(-f.e2[0], cx, __builtin_fmaf(-f.e2[1], cy, -(f.e2[2] * cz)));
+    const float Y = __builtin_fmaf(f.e1[0], cx, __builtin_fmaf(f.e1[1], cy, f.e1[2] * cz));
+    const float Z = __builtin_fmaf(-sx, f.n[0], __builtin_fmaf(-sy, f.n[1], -(sz * f.n[2])));
+    // the bounds: magnitudes of the record (rounded up by their products' slack), then E = K P
+    const float me1 = fmaxf(fabsf(f.e1[0]), fmaxf(fabsf(f.e1[1]), fabsf(f.e1[2])));
+    const float me2 = fmaxf(fabsf(f.e2[0]), fmaxf(fabsf(f.e2[1]), fabsf(f.e2[2])));
+    const float m0 = fmaxf(fabsf(f.v0[0]), fmaxf(fabsf(f.v0[1]), fabsf(f.v0[2])));
+    const float msk = (r.mo + m0) * 0x5p-20f, mdmsk = r.md * msk, m12 = me1 * me2;
+    const float EX = me2 * mdmsk, EY = me1 * mdmsk, Ea = m12 * r.mdK, EZ = m12 * msk;
+    const float aa = fabsf(A);
+    const float xs = copysignf(1.0f, A) * X, ys = copysignf(1.0f, A) * Y, zs = copysignf(1.0f, A) * Z;
+    const bool r0 = aa + Ea < 0.99999e-4f;
+    const bool r1 = xs < -EX, r2 = ys < -EY;
+    const float W = (xs + ys) - aa;
+    const bool r4 = W > __builtin_fmaf(0x1p-22f, fabsf(W) + aa, (EX + EY) + Ea);
+    const float G = __builtin_fmaf(-0.00099999f, aa, zs);
+    const bool r5 = G + __builtin_fmaf(0x1p-22f, fabsf(G), __builtin_fmaf(0.00099999f, Ea, EZ)) < 0.0f;
+    const float G2 = __builtin_fmaf(-tl, aa, zs);
+    const bool r6 = G2 - __builtin_fmaf(0x1p-22f, fabsf(G2), __builtin_fmaf(tl, Ea, EZ)) > 0.0f;
+    return !(r0 || (aa > Ea && (r1 || r2 || r4 || r5 || r6)));
 }
 
 // bvh_conservative_bound.  A primitive accepted at parameter t has its computed hit point within
@@ -732,6 +829,37 @@ RT_HD void tri_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R tmin, Cl
     for (int k = first; k < end; ++k) {
         const TriLeaf<R> L = sc.bvh_tri_leaf[k];
         R t;
+        RT_HCOUNT(HC_TRI_TESTS, 1);
+        if (!triangle_candidate(L.t, o, d, tmin, t)) continue;
+        if (better(t, L.obj, L.id, b)) {
+            b = Closest<R>{t, HIT_TRI, L.id, sc.tri_mat[L.id], L.obj};
+            tl = bvh_tlimit(b.t);
+        }
+    }
+}
+
+// RT_TRI_FILTER (binary64): a leaf's triangles first through the binary32 pre-filter (48-B records,
+// tri_filter_bound) into a mask of survivors, then the binary64 test over the survivors only, reading
+// their 80-B records — the mirror of the sphere survivor masks (RT_GRID_COMPACT).  Same decisions as
+// tri_leaf (the filter rejects only what the binary64 test rejects; `better` is a total order, so the
+// survivors' order does not matter).  0: every triangle through the binary64 test (A/B).
+#ifndef RT_TRI_FILTER
+#define RT_TRI_FILTER 1
+#endif
+template <class R>
+RT_HD void tri_leaf_filtered(const SceneView<R>& sc, int fc, const TriRay& tr, V3<R> o, V3<R> d, R tmin,
+                             Closest<R>& b, float& tl, Work& w) {
+    const int first = fc >> 4, n = fc & 15;
+    RT_COUNT(w.tris += n);
+    uint32_t pass = 0;
+    for (int i = 0; i < n; ++i)
+        if (tri_filter_pass(sc.tri_filter[first + i], tr, tl)) pass |= 1u << i;
+    while (pass) {
+        const int k = first + __builtin_ctz(pass);
+        pass &= pass - 1;
+        const TriLeaf<R> L = sc.bvh_tri_leaf[k];
+        R t;
+        RT_HCOUNT(HC_TRI_TESTS, 1);
         if (!triangle_candidate(L.t, o, d, tmin, t)) continue;
         if (better(t, L.obj, L.id, b)) {
             b = Closest<R>{t, HIT_TRI, L.id, sc.tri_mat[L.id], L.obj};
@@ -764,8 +892,14 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
             bvh_walk<WIDE, LDSN>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w, leaf);
     }
     if (TRI && sc.num_tri_nodes > 0) {
-        auto leaf = [&](int fc) { tri_leaf(sc, fc, o, d, tmin, b, tl, w); };
-        bvh_walk<WIDE>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, leaf);
+        if constexpr (sizeof(R) == 8 && RT_TRI_FILTER != 0) {
+            const TriRay tr = make_tri_ray(o, d);
+            auto leaf = [&](int fc) { tri_leaf_filtered(sc, fc, tr, o, d, tmin, b, tl, w); };
+            bvh_walk<WIDE>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, leaf);
+        } else {
+            auto leaf = [&](int fc) { tri_leaf(sc, fc, o, d, tmin, b, tl, w); };
+            bvh_walk<WIDE>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, leaf);
+        }
     }
     return b;
 }

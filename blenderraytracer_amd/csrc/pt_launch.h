@@ -34,6 +34,7 @@ struct Counters {
     // the batch's reduce once it is set, and its gate commits the batch only if it is set)
     uint32_t* batch_count = nullptr;
     uint32_t* batch_flag = nullptr;
+    int flag_stride = 1;       // the flag of the launch's batch b at batch_flag[b * flag_stride]
 };
 constexpr int kCancelCopies = 128, kCancelStride = 32;
 
@@ -72,8 +73,8 @@ hipError_t launch_trace_partials(const SceneView<R>& sc, const ImageParams& im, 
 hipError_t launch_reduce(const ImageParams& im, double* sum, const double* part, bool tri_bvh, hipStream_t stream,
                          const ReduceGate* gate = nullptr);
 // All batches of a progressive render in ONE pool launch (items batch-major in the pool's queue): batch
-// b = samples [im.s_begin + b * batch, ...) into part + b * fused_batch_doubles(...), each batch's items
-// signalled through c.batch_count / c.batch_flag.  The same items, chunks and partials as one
+// b = samples [im.s_begin + b * stride, + batch) (stride = im.batch_stride, or batch) into part + b *
+// fused_batch_doubles(...), each batch's items signalled through c.batch_count / c.batch_flag.  The same items, chunks and partials as one
 // launch_trace_partials per batch, so launch_reduce of each batch's partials adds the same bits.
 template <class R>
 hipError_t launch_trace_batches(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh, int batch,
@@ -108,10 +109,13 @@ struct FinalizeParams {
     int tone_map;
     double exposure, gamma;
 };
-// preview: a running frame of a progressive render (RGBA8 only): preview_kernel, whose gamma pow is
-// binary32 (within one RGBA8 step of the exact frame on rare pixels; pt_trace.hip)
+// thresholds: a running frame of a progressive render (RGBA8 only) through preview_kernel, whose bytes
+// come from the 255 gamma thresholds of launch_gamma_thresholds instead of a binary64 pow (the same
+// bytes as finalize_kernel in 29 VGPRs, so it runs beside the trace waves; pt_trace.hip)
 hipError_t launch_finalize(const FinalizeParams& p, const double* sum, double* mean, float* post, uint8_t* rgba8,
-                           hipStream_t stream, bool preview = false);
+                           hipStream_t stream, const double* thresholds = nullptr);
+bool preview_thresholds_ok(double gamma);
+hipError_t launch_gamma_thresholds(double gamma, double* T, hipStream_t stream);
 hipError_t launch_denoise(int w, int h, double w1, double w2, const float* in, float* out, uint8_t* rgba8,
                           hipStream_t stream);
 

@@ -139,16 +139,45 @@ __device__ __forceinline__ void store_through(double* p, double v) {
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The wave's item of a fused launch is done: once its partials' stores have completed (vmcnt(0), as
-// inline asm, which the compiler cannot drop), lane 0 counts the item for its batch, and the lane whose
-// count completes the batch raises the batch's flag in mapped host memory (the host then enqueues the
-// batch's reduce, a later kernel launch, so the reads need no acquire of their own)
+// The wave's item of a fused launch is done (the commit protocol of fused batches).  The
+// happens-before chain from a wave's partial stores to the reduce that reads them on another stream:
+//  1. every lane: its partial stores, then an agent-scope release fence (the lanes of a wave are one
+//     instruction stream: the fence orders the wave's stores before lane 0's increment below);
+//  2. lane 0: the batch's item count, a relaxed agent-scope RMW after that fence — the counts of a batch's
+//     items form one release sequence headed by every item's fenced increment;
+//  3. the lane whose increment completes the batch: an agent-scope acquire fence (it has read the last
+//     value of that sequence, so it synchronizes with every other item's release), then the batch's flag
+//     in mapped host memory, a system-scope release store;
+//  4. the host sees the flag and enqueues the batch's gate, which loads the flag with a system-scope
+//     acquire (reduce_gate_kernel) before it lets the reduce run; the reduce follows the gate in stream
+//     order.
+// On gfx950 the release fence is an L2 write-back (buffer_wbl2 sc1) + vmcnt(0) per item (one; an acq_rel
+// RMW would add a second write-back and an invalidate).  RT_COMMIT_FENCE: 2 (A/B) the acq_rel RMW form;
+// 0 (A/B) round 4's form — an inline `s_waitcnt vmcnt(0)` after the stores and relaxed atomics, correct on
+// gfx950 only because the partial stores are written through (sc1) and complete at the wait
+#ifndef RT_COMMIT_FENCE
+#define RT_COMMIT_FENCE 1
+#endif
 __device__ __forceinline__ void item_done(const Counters& c, int b, uint32_t batch_items, int lane) {
+#if RT_COMMIT_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+        const uint32_t k = __hip_atomic_fetch_add(c.batch_count + b, 1u, RT_COMMIT_FENCE == 2 ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        if (k + 1 == batch_items) {
+            if (RT_COMMIT_FENCE != 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __hip_atomic_store(c.batch_flag + b * c.flag_stride, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+#else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) {
         const uint32_t k = __hip_atomic_fetch_add(c.batch_count + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (k + 1 == batch_items) __hip_atomic_store(c.batch_flag + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (k + 1 == batch_items)
+            __hip_atomic_store(c.batch_flag + b * c.flag_stride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+#endif
 }
 
 // ---- lane-per-pixel kernel (RT_SAMPLE_POOL=0) ----
@@ -637,7 +666,9 @@ __global__ __launch_bounds__(64) void reduce_gate_kernel(const ReduceGate g) {
     if (threadIdx.x != 0) return;
     const uint32_t a = __hip_atomic_load(const_cast<uint32_t*>(g.aborted), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint32_t s = __hip_atomic_load(g.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint32_t f = g.complete ? __hip_atomic_load(g.complete, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 1u;
+    // a fused batch's flag: the acquire end of item_done's release chain (the partials the reduce reads)
+    const uint32_t f = g.complete ? __hip_atomic_load(g.complete, RT_COMMIT_FENCE ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_SYSTEM) : 1u;
     const uint32_t skip = (a | s) || !f ? 1u : 0u;
     *g.skip = skip;
     if (skip) __hip_atomic_store(g.stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -645,12 +676,11 @@ __global__ __launch_bounds__(64) void reduce_gate_kernel(const ReduceGate g) {
 }
 
 bool trace_uses_pool() {
-    static int v = -1;
-    if (v == -1) {
+    static const bool v = [] {             // thread-safe initialization (renders on several threads)
         const char* e = getenv("RT_SAMPLE_POOL");
-        v = !(e && e[0] == '0');
-    }
-    return v == 1;
+        return !(e && e[0] == '0');
+    }();
+    return v;
 }
 
 // Samples per pool wave: ~2 sqrt(ns) (0.75 sqrt(ns) when the scene has a triangle BVH: its walks
@@ -663,11 +693,10 @@ bool trace_uses_pool() {
 // 6947; 4K x 128 c23 / c45 7331 / 7393; mesh50k 256 spp c12 / c16 / c24 / c32 6786 / 6673 / 6687 /
 // 6391; Cornell 512^2 x 64 spp (4096 tiles) 4.  RT_POOL_CHUNK overrides (A/B runs).
 static int pool_chunk(int ns, int tiles, bool tri_bvh) {
-    static int v = -1;
-    if (v == -1) {
+    static const int v = [] {
         const char* e = getenv("RT_POOL_CHUNK");
-        v = e ? std::max(1, atoi(e)) : 0;
-    }
+        return e ? std::max(1, atoi(e)) : 0;
+    }();
     if (v) return v;
     int c = std::min(128, std::max(4, (int)((tri_bvh ? 0.75 : 2.0) * std::sqrt((double)ns) + 0.5)));
     const int cmax = tri_bvh ? c : std::min(128, std::max(4, (int)(4.0 * std::sqrt((double)ns) + 0.5)));
@@ -717,11 +746,10 @@ size_t pool_partial_bytes(int cw, int ch, int ns, bool tri_bvh, int chunk_overri
 #endif
 template <class R>
 static size_t lds_grid_bytes(const SceneView<R>& sc) {
-    static int v = -1;
-    if (v == -1) {
+    static const int v = [] {
         const char* e = getenv("RT_LDS_GRID");
-        v = e ? atoi(e) : RT_LDS_GRID;
-    }
+        return e ? atoi(e) : RT_LDS_GRID;
+    }();
     if (v < 1 || sc.num_grid_cells <= 0) return 0;
     constexpr int W = lds_waves<R, ACC_GRID_LDS>();
     const size_t b = ((grid_lds_bytes(sc) + 15) & ~(size_t)15) + (RT_MAT_LDS ? sizeof(MatRec<R>) * (size_t)sc.num_mats : 0);
@@ -734,11 +762,10 @@ static size_t lds_grid_bytes(const SceneView<R>& sc) {
 // not fit: the kernel's workgroups per CU share its 160 KiB
 template <class R>
 static size_t lds_nodes_bytes(const SceneView<R>& sc) {
-    static int v = -1;
-    if (v == -1) {
+    static const int v = [] {
         const char* e = getenv("RT_LDS_NODES");
-        v = e ? atoi(e) : RT_LDS_NODES;
-    }
+        return e ? atoi(e) : RT_LDS_NODES;
+    }();
     if (v < (sizeof(R) == 8 ? 2 : 1) || sc.num_sphere_wide <= 0) return 0;
     constexpr int W = lds_waves<R>();
     const size_t b = (size_t)56 * sc.num_sphere_wide + (size_t)W * std::min(sc.stack_entries, RT_BVH_STACK) * 64 * 4;
@@ -751,16 +778,22 @@ static size_t lds_nodes_bytes(const SceneView<R>& sc) {
 static std::atomic<unsigned> g_next_queue{0};
 
 static int device_cus() {
-    static int cus[64] = {0};
+    static std::atomic<int> cus[64];       // 0: not yet read (racing readers store the same value)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus[dev] = 256;
-    return cus[dev];
+    int n = cus[dev].load(std::memory_order_relaxed);
+    if (!n) {
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cus[dev].store(n, std::memory_order_relaxed);
+    }
+    return n;
 }
 
 template <class R, int ACC>
-static void launch_pool_kernel(const TraceArgs<R>& a, bool count, double* part, int tiles, int chunks, int chunk,
+static void launch_pool_kernel(const TraceArgs<R>& a0, bool count, double* part, int tiles, int chunks, int chunk,
                                hipStream_t stream) {
+    TraceArgs<R> a = a0;
+    if (a.im.order_chunk0 < 0) a.im.order_chunk0 = chunks - 1;   // the tile order for the last chunk only
     if constexpr (ACC == ACC_BVH_SPHERES || ACC == ACC_GRID) {
         constexpr int LACC = ACC == ACC_GRID ? ACC_GRID_LDS : ACC_BVH_SPHERES_LDS;
         const size_t lb = ACC == ACC_GRID ? lds_grid_bytes(a.sc) : lds_nodes_bytes(a.sc);
@@ -826,14 +859,13 @@ static hipError_t launch_pool(const TraceArgs<R>& a0, bool count, hipStream_t st
 // sphere-only form for scenes without triangles (RT_BVH_WALK=two: always the general form)
 template <class R>
 static int bvh_walk_mode(const SceneView<R>& sc) {
-    static int v = -1;
-    if (v == -1) {
+    static const int v = [] {
         const char* e = getenv("RT_BVH_WALK");
         // A/B: skip = stackless walk, two = the general ordered walk, tree = the sphere tree even where
         // the grid was chosen, grid = the grid wherever one was built
-        v = e && !strncmp(e, "skip", 4) ? ACC_BVH : e && !strncmp(e, "two", 3) ? ACC_BVH_STACK
-          : e && !strncmp(e, "grid", 4) ? ACC_GRID : e && !strncmp(e, "tree", 4) ? -2 : ACC_BVH_SPHERES;
-    }
+        return e && !strncmp(e, "skip", 4) ? ACC_BVH : e && !strncmp(e, "two", 3) ? ACC_BVH_STACK
+             : e && !strncmp(e, "grid", 4) ? ACC_GRID : e && !strncmp(e, "tree", 4) ? -2 : ACC_BVH_SPHERES;
+    }();
     if (sc.num_tri_nodes > 0) return v == ACC_BVH ? ACC_BVH : ACC_BVH_STACK;
     const bool grid = sc.num_grid_cells > 0 && (v == ACC_GRID || (v == ACC_BVH_SPHERES && sc.use_grid));
     return grid ? ACC_GRID : v == -2 || v == ACC_GRID ? ACC_BVH_SPHERES : v;
@@ -926,7 +958,9 @@ hipError_t launch_trace_batches(const SceneView<R>& sc, const ImageParams& im0, 
     if (im0.cw <= 0 || im0.ch <= 0 || im0.s_end <= im0.s_begin || batch <= 0) return hipSuccess;
     const bool tri = sc.num_tri_nodes > 0;
     const PoolPlan p = pool_plan(im0.cw, im0.ch, batch, tri, im0.pool_chunk);   // one batch's chunks
-    const int nb = (im0.s_end - im0.s_begin + batch - 1) / batch;
+    const int stride = im0.batch_stride > 0 ? im0.batch_stride : batch;
+    if (stride < batch) return hipErrorInvalidValue;
+    const int nb = (im0.s_end - im0.s_begin + stride - 1) / stride;
     if (!part || !c.batch_count || !c.batch_flag || part_bytes < (size_t)nb * p.part_bytes) return hipErrorInvalidValue;
     if ((long long)p.tiles * p.chunks * nb > 0x7FFFFFFFLL) return hipErrorInvalidConfiguration;
     ImageParams im = im0;
@@ -1101,15 +1135,35 @@ __global__ __launch_bounds__(64) void finalize_kernel(const FinalizeParams p, co
 // The running frame of a progressive render (RGBA8 only) in at most 32 VGPRs: while batches trace, the
 // trace waves hold 480 of a SIMD's 512 VGPRs (5 waves x 96), and finalize_kernel's 80-VGPR waves wait
 // for trace waves to exit (measured 0.2 - 7.5 ms per preview, delaying the next batches' reduces on the
-// same stream; a fused launch's waves never exit).  The binary64 pow alone needs 64 VGPRs, so the gamma
-// pow here is binary32 (28 VGPRs): the frame is within one RGBA8 step of finalize_kernel's on pixels
-// whose value lies within ~1e-7 of a rounding boundary.  The final frame and a cancelled render's frame
-// come from finalize_kernel.
+// same stream; a fused launch's waves never exit).  The binary64 pow alone needs 64 VGPRs, so the
+// preview does without it: the byte finalize_kernel stores, floor(255 pow(max(0, tm), 1/gamma)) clamped,
+// is a non-decreasing step function of the tone-mapped value tm, so it equals the number of thresholds
+// T_k <= tm, T_k (k = 1..255) the least binary64 tm whose byte is >= k — computed once per gamma by
+// gamma_thresholds_kernel with the device's own binary64 pow (finalize_kernel's).  The preview computes
+// tm exactly as finalize_kernel (binary64, same operations) and counts the thresholds by binary search:
+// the same bytes (tests/test_gpu_parity.py::test_progressive_preview_and_cancel, and the threshold
+// neighbourhoods in ::test_preview_thresholds_match_finalize).  NaN tm: byte 0, as to_u8.
+__device__ __forceinline__ uint32_t gamma_byte(double tm, double inv_gamma) {
+    return to_u8(pow(js_max<double>(0.0, tm), inv_gamma));
+}
+__global__ __launch_bounds__(256) void gamma_thresholds_kernel(const double inv_gamma, double* __restrict__ T) {
+    const uint32_t k = threadIdx.x + 1;
+    if (k > 255) return;
+    // smallest non-negative binary64 tm (by bit pattern, the same order) with byte(tm) >= k:
+    // byte(+0) = 0 < k, byte(+inf) = 255 >= k
+    uint64_t lo = 0, hi = 0x7FF0000000000000ull;
+    while (hi - lo > 1) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (gamma_byte(__longlong_as_double((long long)mid), inv_gamma) >= k) hi = mid;
+        else lo = mid;
+    }
+    T[k - 1] = __longlong_as_double((long long)hi);
+}
+
 __global__ __launch_bounds__(64) void preview_kernel(const FinalizeParams p, const double* __restrict__ sum,
-                                                     uint8_t* __restrict__ rgba8) {
+                                                     const double* __restrict__ T, uint8_t* __restrict__ rgba8) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= p.n) return;
-    const float inv_gamma = (float)(1.0 / p.gamma);
     uint32_t o = 255u << 24;
 #pragma unroll 1
     for (int k = 0; k < 3; ++k) {
@@ -1118,16 +1172,34 @@ __global__ __launch_bounds__(64) void preview_kernel(const FinalizeParams p, con
         if (p.tone_map == 1) tm = js_max<double>(0.0, (x * (2.51 * x + 0.03)) / (x * (2.43 * x + 0.59) + 0.14));
         else if (p.tone_map == 2) tm = x;
         else tm = x / (1.0 + x);
-        o |= (uint32_t)to_u8((double)powf((float)js_max<double>(0.0, tm), inv_gamma)) << (8 * k);
+        // the number of thresholds <= tm (T ascending; a NaN tm passes none)
+        uint32_t lo = 0, n = 255;
+        while (n > 0) {
+            const uint32_t h = n >> 1;
+            if (T[lo + h] <= tm) { lo += h + 1; n -= h + 1; }
+            else n = h;
+        }
+        o |= lo << (8 * k);
     }
     *reinterpret_cast<uint32_t*>(rgba8 + 4 * q) = o;
 }
 
+// thresholds of gamma_byte for this gamma (255 doubles); false when 1/gamma is not a finite positive
+// number (the byte is then not a non-decreasing function of tm, and previews take finalize_kernel)
+bool preview_thresholds_ok(double gamma) {
+    const double ig = 1.0 / gamma;
+    return ig > 0.0 && ig < INFINITY;
+}
+hipError_t launch_gamma_thresholds(double gamma, double* T, hipStream_t stream) {
+    hipLaunchKernelGGL(gamma_thresholds_kernel, dim3(1), dim3(256), 0, stream, 1.0 / gamma, T);
+    return hipGetLastError();
+}
+
 hipError_t launch_finalize(const FinalizeParams& p, const double* sum, double* mean, float* post, uint8_t* rgba8,
-                           hipStream_t stream, bool preview) {
+                           hipStream_t stream, const double* thresholds) {
     if (p.n <= 0) return hipSuccess;
-    if (preview && !mean && !post && rgba8)
-        hipLaunchKernelGGL(preview_kernel, dim3((p.n + 63) / 64), dim3(64), 0, stream, p, sum, rgba8);
+    if (thresholds && !mean && !post && rgba8)
+        hipLaunchKernelGGL(preview_kernel, dim3((p.n + 63) / 64), dim3(64), 0, stream, p, sum, thresholds, rgba8);
     else
         hipLaunchKernelGGL(finalize_kernel, dim3((p.n + 63) / 64), dim3(64), 0, stream, p, sum, mean, post, rgba8);
     return hipGetLastError();

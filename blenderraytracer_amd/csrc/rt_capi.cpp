@@ -99,6 +99,7 @@ struct DeviceScene {
     DevBuf<BvhNode> sphere_nodes, tri_nodes;
     DevBuf<SphereLeaf<R>> bvh_sphere_leaf;
     DevBuf<TriLeaf<R>> bvh_tri_leaf;
+    DevBuf<TriFilter> tri_filter;
     DevBuf<SphereLeaf<R>> big_sphere_leaf;
     DevBuf<Bvh2Node> sphere_wide, tri_wide;
     DevBuf<int> grid_cell;
@@ -108,7 +109,7 @@ struct DeviceScene {
         runs.release(); spheres.release(); sphere_filter.release(); sphere_r.release(); sphere_inv_r.release(); planes.release(); boxes.release(); tris.release();
         sphere_mat.release(); plane_mat.release(); box_mat.release(); tri_mat.release(); perm.release(); mats.release();
         plane_obj.release(); box_obj.release(); sphere_nodes.release(); tri_nodes.release(); bvh_sphere_leaf.release();
-        bvh_tri_leaf.release(); big_sphere_leaf.release();
+        bvh_tri_leaf.release(); tri_filter.release(); big_sphere_leaf.release();
         sphere_wide.release(); tri_wide.release(); grid_cell.release(); grid_leaf.release();
     }
 };
@@ -123,7 +124,7 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     UP(boxes, rec.boxes); UP(tris, rec.tris); UP(sphere_mat, hs.sphere_mat); UP(plane_mat, hs.plane_mat);
     UP(box_mat, hs.box_mat); UP(tri_mat, hs.tri_mat); UP(perm, rec.perm); UP(mats, rec.mats);
     UP(plane_obj, hs.plane_obj); UP(box_obj, hs.box_obj); UP(sphere_nodes, hs.sphere_bvh); UP(tri_nodes, hs.tri_bvh);
-    UP(bvh_sphere_leaf, rec.bvh_sphere_leaf); UP(bvh_tri_leaf, rec.bvh_tri_leaf); UP(big_sphere_leaf, rec.big_sphere_leaf); UP(sphere_wide, hs.sphere_wide); UP(tri_wide, hs.tri_wide);
+    UP(bvh_sphere_leaf, rec.bvh_sphere_leaf); UP(bvh_tri_leaf, rec.bvh_tri_leaf); UP(tri_filter, rec.tri_filter); UP(big_sphere_leaf, rec.big_sphere_leaf); UP(sphere_wide, hs.sphere_wide); UP(tri_wide, hs.tri_wide);
     UP(grid_cell, hs.grid_cell); UP(grid_leaf, rec.grid_leaf);
 #undef UP
     if (e != hipSuccess) return fail(RT_ERR_DEVICE, "scene upload: %s", hipGetErrorString(e));
@@ -133,7 +134,7 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     v.tris = ds.tris.p; v.sphere_mat = ds.sphere_mat.p; v.plane_mat = ds.plane_mat.p; v.box_mat = ds.box_mat.p;
     v.tri_mat = ds.tri_mat.p; v.mats = ds.mats.p; v.perm = ds.perm.p;
     v.plane_obj = ds.plane_obj.p; v.box_obj = ds.box_obj.p; v.sphere_nodes = ds.sphere_nodes.p; v.tri_nodes = ds.tri_nodes.p;
-    v.bvh_sphere_leaf = ds.bvh_sphere_leaf.p; v.bvh_tri_leaf = ds.bvh_tri_leaf.p;
+    v.bvh_sphere_leaf = ds.bvh_sphere_leaf.p; v.bvh_tri_leaf = ds.bvh_tri_leaf.p; v.tri_filter = ds.tri_filter.p;
     v.big_spheres = ds.big_sphere_leaf.p;
     v.sphere_wide = ds.sphere_wide.p; v.tri_wide = ds.tri_wide.p;
     v.grid_cell = ds.grid_cell.p; v.grid_leaf = ds.grid_leaf.p;
@@ -201,6 +202,9 @@ struct DeviceState {
     DevBuf<double> fused_part;
     DevBuf<uint32_t> fused_count;
     hipEvent_t fused_done = nullptr;
+    // the pool's longest-first tile order of the last crop (tile_order) and that crop's key
+    DevBuf<int> tile_order;
+    int order_key[6] = {-1, -1, -1, -1, -1, -1};
 
     int init(int dev, const HostScene& hs, const rt_scene_desc& d) {
         device = dev;
@@ -236,7 +240,7 @@ struct DeviceState {
         s64.release();
         s32.release();
         sum.release(); segs.release(); draws.release(); total.release(); part.release(); gate_skip.release();
-        fused_part.release(); fused_count.release();
+        fused_part.release(); fused_count.release(); tile_order.release();
         for (DevBuf<double>& b : part_more) b.release();
         for (hipEvent_t e : {ev[0], ev[1], setup_ev, scratch_ev, copy_ev, fused_done})
             if (e) (void)hipEventDestroy(e);
@@ -310,6 +314,8 @@ struct rt_scene {
     std::vector<uint8_t*> preview_dev;    // the same buffers' device addresses
     size_t preview_host_n = 0;
     std::vector<hipEvent_t> batch_done;   // home stream: batch k's reduce, merges and preview done (slot k % ring)
+    DevBuf<double> gamma_t;         // preview frames: the 255 RGBA8 thresholds of gamma gamma_t_of (launch_gamma_thresholds)
+    double gamma_t_of = NAN;
     std::atomic<int> cancel{0};
     uint32_t* ctl = nullptr;        // the render's control words (kCtl*), host address
     uint32_t* ctl_dev = nullptr;    // ... their device address (portable mapping: valid on every device)
@@ -345,10 +351,21 @@ int check_settings(const rt_settings* s, int* cw, int* ch) {
     return RT_OK;
 }
 
-// mean, toneMap, gammaCorrect (+ PostProcessor.denoise), RGBA8 on `st` (ray-tracer.js:208-276)
+// mean, toneMap, gammaCorrect (+ PostProcessor.denoise), RGBA8 on `st` (ray-tracer.js:208-276).
+// thresholds: an RGBA8-only epilogue through the gamma thresholds (preview_kernel: the same bytes, 29
+// VGPRs instead of finalize_kernel's 80); the table is built, once per gamma, on `st` and waited for
 hipError_t epilogue(rt_scene* sc, const rt_settings* s, int cw, int ch, const double* sum, double* mean, float* post,
-                    uint8_t* rgba, hipStream_t st) {
+                    uint8_t* rgba, hipStream_t st, bool thresholds = false) {
     FinalizeParams fp{cw * ch, s->samples, s->tone_map, s->exposure, s->gamma};
+    if (thresholds && !s->denoise && !mean && !post && rgba && preview_thresholds_ok(s->gamma)) {
+        hipError_t e = sc->gamma_t.ensure(255);
+        if (e == hipSuccess && !(sc->gamma_t_of == s->gamma)) {
+            e = launch_gamma_thresholds(s->gamma, sc->gamma_t.p, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e == hipSuccess) sc->gamma_t_of = s->gamma;
+        }
+        return e == hipSuccess ? launch_finalize(fp, sum, nullptr, nullptr, rgba, st, sc->gamma_t.p) : e;
+    }
     if (!s->denoise) return launch_finalize(fp, sum, mean, post, rgba, st);
     hipError_t e = sc->post_raw.ensure(4 * (size_t)cw * ch);
     if (e == hipSuccess) e = launch_finalize(fp, sum, mean, sc->post_raw.p, nullptr, st);
@@ -383,6 +400,58 @@ int check_accel(const rt_scene* sc, const rt_settings* s) {
         return fail(RT_ERR_INVALID, "BVH deeper than the %d-entry traversal stack (too many primitives): use "
                     "RT_ACCEL_AUTO or RT_ACCEL_BRUTE", RT_BVH_STACK);
     return RT_OK;
+}
+
+// The pool's longest-first tile order (pool_order.h item_at): a launch's items taken in raster order end
+// on whatever tiles come last, and its waves drain over the longest of them — config 3's 64-spp share
+// of 8 GPUs measured 6 % below the full frame's rate.  The crop's tiles sorted by the estimated cost of
+// their region (estimate_costs, scene_pack.h), most expensive first (ragged tiles scaled by their pixel
+// count, ties in raster order), so that each chunk of the launch ends on its cheapest tiles.  Only the
+// visiting order changes: the same items, partials and sums.  RT_TILE_LPT (A/B): 0 never (default: on
+// config 3 the order measured 1.6 % slower at 64 spp per rank and 0.3 % at 512 spp, DESIGN.md §4 — the
+// in-flight items lose their screen locality), 1 scenes walked through the grid (the LDS pool kernel's
+// device-wide queue), 2 every BVH scene, 3 grid scenes and only the launch's last chunk (the tail).
+int tile_order_mode() {
+    static const int v = [] {
+        const char* e = getenv("RT_TILE_LPT");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
+std::vector<int> tile_order_host(const HostScene& hs, const ImageParams& im) {
+    const int tx = (im.cw + 7) / 8, ty = (im.ch + 7) / 8;
+    std::vector<float> cost((size_t)tx * ty);
+    for (int t = 0; t < tx * ty; ++t) {
+        const int x0 = (t % tx) * 8, y0 = (t / tx) * 8;
+        const int vw = std::min(8, im.cw - x0), vh = std::min(8, im.ch - y0);
+        const double X = im.x0 + x0 + 0.5 * vw, Y = im.y0 + y0 + 0.5 * vh;      // tile centre, top-down rows
+        const int i = std::min(kCostNX - 1, (int)(X * kCostNX / im.width));
+        const int r = std::min(kCostNY - 1, (int)(Y * kCostNY / im.height));
+        cost[t] = hs.cost[(size_t)r * kCostNX + i] * (float)(vw * vh);
+    }
+    std::vector<int> order(cost.size());
+    for (size_t t = 0; t < order.size(); ++t) order[t] = (int)t;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+    return order;
+}
+
+hipError_t scratch_idle(DeviceState& ds);
+
+// the device copy of the order for this crop (nullptr: raster order), re-uploaded when the crop changes
+const int* tile_order(const rt_scene* sc, DeviceState& ds, const ImageParams& im) {
+    if (sc->hs.cost.empty() || im.cw <= 0 || im.ch <= 0) return nullptr;
+    const int key[6] = {im.width, im.height, im.x0, im.y0, im.cw, im.ch};
+    if (ds.tile_order.p && std::equal(key, key + 6, ds.order_key)) return ds.tile_order.p;
+    const std::vector<int> order = tile_order_host(sc->hs, im);
+    if (scratch_idle(ds) != hipSuccess || ds.tile_order.ensure(order.size()) != hipSuccess ||
+        hipMemcpy(ds.tile_order.p, order.data(), order.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipGetLastError();
+        std::fill(ds.order_key, ds.order_key + 6, -1);
+        return nullptr;                              // raster order: slower only
+    }
+    std::copy(key, key + 6, ds.order_key);
+    return ds.tile_order.p;
 }
 
 // rt_settings.sum_order: the sample pool unless the caller asks for sample order (or RT_SAMPLE_POOL=0)
@@ -508,11 +577,10 @@ int enable_peer(int a, int b) {
 // chunks as fit (launch_trace then splits the samples over several launches).  RTOW 1080p x 512 spp
 // needs 0.3 GB; a launch with a single chunk needs none.  Kept by the device state between renders.
 size_t part_budget() {
-    static size_t budget = 0;
-    if (!budget) {
+    static const size_t budget = [] {
         const char* e = getenv("RT_PART_MB");
-        budget = (size_t)(e ? std::max(1LL, atoll(e)) : 2048LL) << 20;
-    }
+        return (size_t)(e ? std::max(1LL, atoll(e)) : 2048LL) << 20;
+    }();
     return budget;
 }
 
@@ -577,11 +645,10 @@ bool ensure_fused(DeviceState& ds, size_t doubles, int nb) {
     const size_t bytes = doubles * (size_t)nb * sizeof(double);
     if (bytes == 0) return false;
     if (ds.fused_part.n * sizeof(double) < bytes) {
-        static size_t budget = 0;
-        if (!budget) {
+        static const size_t budget = [] {   // thread-safe initialization (concurrent renders of other scenes)
             const char* e = getenv("RT_FUSED_MB");
-            budget = (size_t)(e ? std::max(0LL, atoll(e)) : 8192LL) << 20;
-        }
+            return (size_t)(e ? std::max(0LL, atoll(e)) : 8192LL) << 20;
+        }();
         size_t free_b = 0, total_b = 0, cap = budget;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = std::min(cap, (free_b + ds.fused_part.n * sizeof(double)) / 10);
         if (bytes > cap) return false;
@@ -719,6 +786,8 @@ int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out) {
     }
     build_bvhs(sc->hs);
     choose_walk(sc->hs, *desc);
+    if (tile_order_mode() == 2 || ((tile_order_mode() == 1 || tile_order_mode() == 3) && sc->hs.use_grid))
+        estimate_costs(sc->hs, *desc);
     sc->desc.set(*desc);
     sc->num_prims = sc->hs.num_prims;
     sc->bvh_prims = (int)(sc->hs.sphere_r.size() + sc->hs.tri_mat.size());
@@ -756,6 +825,7 @@ void rt_scene_destroy(rt_scene* sc) {
     sc->mean.release(); sc->post.release(); sc->post_raw.release();
     for (MergeSlot& m : sc->merge) m.release();
     sc->rgba.release();
+    sc->gamma_t.release();
     for (uint8_t* p : sc->preview_host)
         if (p) (void)hipHostFree(p);
     if (sc->ctl) (void)hipHostFree(sc->ctl);
@@ -824,7 +894,8 @@ int merge_shards(rt_scene* sc, const std::vector<DeviceState*>& states, size_t n
     return RT_OK;
 }
 
-// rt_render and rt_render_resume: trace samples [first, sample_end) on top of `sums_in` (NULL: zeros).
+// rt_render and rt_render_resume: trace samples [first, sample_end) on top of `sums_in` (NULL: zeros;
+// `resident`: the sums the scene's home device already holds, its checkpoint).
 //
 // Batches (rt_settings.batch_samples) are pipelined: batch k+1 is enqueued before the host waits for
 // batch k, so the GPU never idles on the host's progress call.  With the sample pool and more than one
@@ -837,7 +908,7 @@ int merge_shards(rt_scene* sc, const std::vector<DeviceState*>& states, size_t n
 // observed after a batch, and the batches already queued complete.  Several devices: whole batches
 // round-robin (trace_replica), or every batch split over the devices (merge_shards).
 int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progress_fn progress, void* user,
-                rt_stats* stats, const double* sums_in, int first) {
+                rt_stats* stats, const double* sums_in, int first, bool resident = false) {
     const double t_start = now_ms();
     if (!sc) return fail(RT_ERR_INVALID, "scene is NULL");
     int cw, ch;
@@ -852,6 +923,11 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     const bool want_segs = out && out->segments, want_draws = out && out->draws;
     const bool pool = use_pool(s);
     ImageParams im = image_params(s, cw, ch);
+    if (pool && states.size() == 1 && states[0] == &sc->home) {   // one device: the longest-first tile order
+        HIP_TRY(hipSetDevice(sc->home.device));
+        im.tile_order = tile_order(sc, sc->home, im);
+        im.order_chunk0 = tile_order_mode() == 3 ? -1 : 0;
+    }
     const int base = im.s_begin;                  // the sums hold samples [base, done) of every pixel
     im.s_begin = std::max(im.s_begin, first);
     const int s0 = im.s_begin, s1 = std::max(im.s_end, s0);
@@ -937,16 +1013,22 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     // batch-major in the pool's queue (launch_trace_batches: the same items, chunks and partials as one
     // launch per batch), and each batch's reduce enqueued by the host once the batch's last item has
     // raised its flag — the persistent workgroups never drain between batches (16 batches of config 3
-    // drained for 3.5 % of the trace time).  The reduces (16 VGPRs) and the preview frames (binary32
-    // pow, 28 VGPRs) run beside the trace waves, which leave 32 of a SIMD's 512 VGPRs free.
+    // drained for 3.5 % of the trace time).  The reduces (16 VGPRs) and the preview frames (gamma
+    // thresholds, 29 VGPRs) run beside the trace waves, which leave 32 of a SIMD's 512 VGPRs free.
+    // Several devices (the whole-batch split): device d traces its batches k = d, d + N, ... in one launch
+    // (ImageParams::batch_stride), raising batch k's flag; the host then copies that batch's partials to
+    // the home device and reduces them there in batch order — the copies and reduces of trace_replica,
+    // from one launch per device instead of one per batch.
     int fchunk = 0;
     size_t fdoubles = 0;
-    bool fused = fuse_env && gated && nsh == 1 && !whole && nb > 1 && nb <= kMaxFused && states[0] == &h;
+    bool fused = fuse_env && gated && nb > 1 && nb <= kMaxFused && (whole || (nsh == 1 && states[0] == &h));
     if (fused) {
         fchunk = batch_chunk(0, batch);
         fdoubles = fused_batch_doubles(cw, ch, batch, sc->tri_bvh, fchunk);
-        HIP_TRY(hipSetDevice(h.device));
-        fused = ensure_fused(h, fdoubles, nb);
+        for (int d = 0; d < nsh && fused; ++d) {
+            HIP_TRY(hipSetDevice(states[d]->device));
+            fused = ensure_fused(*states[d], fdoubles, (nb - d + nsh - 1) / nsh);
+        }
     }
     bool fused_launched = false;
     for (int k = 0; k < nsh; ++k) {
@@ -959,7 +1041,9 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         const int ns = std::max(1, b1 - b0);
         if (!overlap && s->max_depth > 0 && (rc = ensure_partials(sc, ds, cw, ch, ns, pool, c, batch_chunk(k, ns)))) return rc;
         HIP_TRY(order_scratch(ds, ds.stream));
-        if (sums_in && &ds == &h)
+        if (resident && &ds == &h) {
+            // the scene's checkpoint is already in place
+        } else if (sums_in && &ds == &h)
             HIP_TRY(hipMemcpyAsync(ds.sum.p, sums_in, 3 * n * sizeof(double), hipMemcpyHostToDevice, ds.stream));
         else
             HIP_TRY(hipMemsetAsync(ds.sum.p, 0, 3 * n * sizeof(double), ds.stream));
@@ -983,7 +1067,9 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     if (states[0] != &h) {                        // the home device only merges: its buffers start here
         HIP_TRY(hipSetDevice(h.device));
         HIP_TRY(h.sum.ensure(3 * n));
-        if (sums_in) HIP_TRY(hipMemcpyAsync(h.sum.p, sums_in, 3 * n * sizeof(double), hipMemcpyHostToDevice, h.stream));
+        if (resident) {
+            // the scene's checkpoint is already in place
+        } else if (sums_in) HIP_TRY(hipMemcpyAsync(h.sum.p, sums_in, 3 * n * sizeof(double), hipMemcpyHostToDevice, h.stream));
         else HIP_TRY(hipMemsetAsync(h.sum.p, 0, 3 * n * sizeof(double), h.stream));
         if (want_segs) {
             HIP_TRY(h.segs.ensure(n));
@@ -1013,6 +1099,17 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
             }
             sc->preview_host_n = 4 * n;
         }
+    }
+    // the running frames' RGBA8 thresholds for this gamma (exact bytes without a binary64 pow: preview_kernel)
+    const double* thresholds = nullptr;
+    if (want_preview && preview_thresholds_ok(s->gamma)) {
+        HIP_TRY(hipSetDevice(h.device));
+        HIP_TRY(sc->gamma_t.ensure(255));
+        if (!(sc->gamma_t_of == s->gamma)) {
+            HIP_TRY(launch_gamma_thresholds(s->gamma, sc->gamma_t.p, h.stream));
+            sc->gamma_t_of = s->gamma;
+        }
+        thresholds = sc->gamma_t.p;
     }
     sc->ckpt_pixels = n;
     sc->ckpt_done = s0;
@@ -1046,41 +1143,80 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
             }
             return c;
         };
-        if (fused) {                              // the render's one launch, then batch kb's reduce
-            HIP_TRY(hipSetDevice(h.device));
+        if (fused) {                              // one launch per device, then batch kb's reduce
             const bool bvh = use_bvh(sc, s);
             if (kb == 0) {
                 for (int k = 0; k < nb; ++k) ctl_store(sc->ctl, kCtlFlag + k, 0);
                 ctl_store(sc->ctl, kCtlFusedAborted, 0);
                 ctl_store(sc->ctl, kCtlFusedAborted + 1, 0);
-                HIP_TRY(hipMemsetAsync(h.fused_count.p, 0, nb * sizeof(uint32_t), h.tstream[0]));
-                Counters c = with_cancel(cs[0]);
-                c.aborted = sc->ctl_dev + kCtlFusedAborted + 1;   // written by skipping waves, read by no gate
-                c.batch_count = h.fused_count.p;
-                c.batch_flag = sc->ctl_dev + kCtlFlag;
-                ImageParams fi = im;
-                fi.s_begin = s0;
-                fi.s_end = s1;
-                fi.pool_chunk = fchunk;
-                const size_t fb = h.fused_part.n * sizeof(double);
-                HIP_TRY(s->precision == RT_PREC_F32
-                            ? launch_trace_batches<float>(h.s32.view, fi, c, bvh, batch, h.fused_part.p, fb, h.tstream[0])
-                            : launch_trace_batches<double>(h.s64.view, fi, c, bvh, batch, h.fused_part.p, fb, h.tstream[0]));
-                HIP_TRY(hipEventRecord(h.fused_done, h.tstream[0]));
+                for (int e = 0; e < nsh; ++e) {   // device e: batches e, e + nsh, ... (all of them when nsh = 1)
+                    DeviceState& de = *states[e];
+                    HIP_TRY(hipSetDevice(de.device));
+                    const int nbe = (nb - e + nsh - 1) / nsh;
+                    HIP_TRY(hipMemsetAsync(de.fused_count.p, 0, nbe * sizeof(uint32_t), de.tstream[0]));
+                    Counters c = with_cancel(cs[e]);
+                    c.aborted = sc->ctl_dev + kCtlFusedAborted + 1;   // written by skipping waves, read by no gate
+                    c.batch_count = de.fused_count.p;
+                    c.batch_flag = sc->ctl_dev + kCtlFlag + e;
+                    c.flag_stride = nsh;
+                    ImageParams fi = im;
+                    fi.s_begin = s0 + e * batch;
+                    fi.s_end = s1;
+                    fi.pool_chunk = fchunk;
+                    fi.batch_stride = nsh * batch;
+                    if (&de != &h) fi.tile_order = nullptr;   // (set for the home device's launches only)
+                    const size_t fb = de.fused_part.n * sizeof(double);
+                    HIP_TRY(s->precision == RT_PREC_F32
+                                ? launch_trace_batches<float>(de.s32.view, fi, c, bvh, batch, de.fused_part.p, fb, de.tstream[0])
+                                : launch_trace_batches<double>(de.s64.view, fi, c, bvh, batch, de.fused_part.p, fb, de.tstream[0]));
+                    HIP_TRY(hipEventRecord(de.fused_done, de.tstream[0]));
+                }
                 fused_launched = true;
             }
+            const int d = kb % nsh, lb = kb / nsh;
+            DeviceState& ds = *states[d];
             // the host waits for batch kb's flag; without it (a cancel: its items stay untraced) the
-            // accumulation stream waits for the launch to end, so the gate reads the final `aborted` words
-            while (!ctl_load(sc->ctl, kCtlFlag + kb) && !sc->cancel.load() && hipEventQuery(h.fused_done) == hipErrorNotReady)
+            // consumer stream waits for the device's launch to end, so the gate reads the final words
+            for (;;) {
+                if (ctl_load(sc->ctl, kCtlFlag + kb) || sc->cancel.load()) break;
+                const hipError_t q = hipEventQuery(ds.fused_done);
+                if (q == hipSuccess) break;
+                if (q != hipErrorNotReady) {      // a device fault, not a cancel: fail with the HIP error
+                    (void)hipGetLastError();
+                    return fail(RT_ERR_DEVICE, "fused batch %d: %s", kb, hipGetErrorString(q));
+                }
                 std::this_thread::sleep_for(std::chrono::microseconds(20));
-            if (!ctl_load(sc->ctl, kCtlFlag + kb)) HIP_TRY(hipStreamWaitEvent(h.stream, h.fused_done, 0));
+            }
+            const bool flagged = ctl_load(sc->ctl, kCtlFlag + kb) != 0;
             ImageParams bi = im;
             bi.s_begin = b;
             bi.s_end = be;
             bi.pool_chunk = fchunk;
-            HIP_TRY(launch_reduce(bi, h.sum.p, h.fused_part.p + (size_t)kb * fdoubles, sc->tri_bvh, h.stream, gp));
+            const double* src = ds.fused_part.p + (size_t)lb * fdoubles;
+            if (&ds == &h) {
+                HIP_TRY(hipSetDevice(h.device));
+                if (!flagged) HIP_TRY(hipStreamWaitEvent(h.stream, h.fused_done, 0));
+                HIP_TRY(launch_reduce(bi, h.sum.p, src, sc->tri_bvh, h.stream, gp));
+            } else {                              // a replica's batch: its partials to the home device first
+                MergeSlot& m = sc->merge[d];
+                const int j = lb % kSlots;
+                const size_t bytes = pool_plan(cw, ch, be - b, sc->tri_bvh, fchunk).part_bytes;
+                HIP_TRY(hipSetDevice(h.device));
+                HIP_TRY(m.stage[j].ensure(fdoubles));
+                if (!m.stage_free[j]) HIP_TRY(hipEventCreateWithFlags(&m.stage_free[j], hipEventDisableTiming));
+                HIP_TRY(hipSetDevice(ds.device));
+                if (!flagged) HIP_TRY(hipStreamWaitEvent(ds.stream, ds.fused_done, 0));
+                if (m.stage_used[j]) HIP_TRY(hipStreamWaitEvent(ds.stream, m.stage_free[j], 0));
+                HIP_TRY(hipMemcpyPeerAsync(m.stage[j].p, h.device, src, ds.device, bytes, ds.stream));
+                HIP_TRY(hipEventRecord(ds.traced[j], ds.stream));
+                HIP_TRY(hipSetDevice(h.device));
+                HIP_TRY(hipStreamWaitEvent(h.stream, ds.traced[j], 0));
+                HIP_TRY(launch_reduce(bi, h.sum.p, m.stage[j].p, sc->tri_bvh, h.stream, gp));
+                HIP_TRY(hipEventRecord(m.stage_free[j], h.stream));
+                m.stage_used[j] = true;
+            }
         }
-        if (whole) {                              // the whole batch on one device, reduced on the home device
+        if (whole && !fused) {                    // the whole batch on one device, reduced on the home device
             const int k = kb % nsh, lj = kb / nsh, j = lj % kSlots;
             DeviceState& ds = *states[k];
             ImageParams bi = im;
@@ -1109,7 +1245,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
             // hipMemcpyAsync here is a blit kernel that waits for wave slots behind the trace waves
             // (measured 7-15 ms per 8-MB frame while batches overlap)
             FinalizeParams fp{(int)n, be - base, s->tone_map, s->exposure, s->gamma};
-            HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview_dev[kb % ring], h.stream, true));
+            HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview_dev[kb % ring], h.stream, thresholds));
         }
         HIP_TRY(hipEventRecord(sc->batch_done[kb % ring], h.stream));
         return RT_OK;
@@ -1146,6 +1282,12 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         if ((status = fill(kb + (fused ? 0 : ahead) + 1))) break;   // fused: enqueue(kb) waits for batch kb
         bool merged = true;
         if ((status = complete(kb, merged))) break;
+        if (!merged && !sc->cancel.load()) {
+            // a gate skipped a batch although nobody cancelled (rt_cancel sets `cancel` before the word the
+            // kernels read): an item-count mismatch or a lost flag — an internal failure, not a cancel
+            status = fail(RT_ERR_DEVICE, "batch %d was not committed (internal error)", kb);
+            break;
+        }
         const int be = sc->ckpt_done;
         if (merged && progress && be < s1 && progress((double)(be - s0) / (double)(s1 - s0), user)) {
             sc->cancel.store(1);
@@ -1189,6 +1331,11 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         g_error = err;
         return status;
     }
+    if (fused_launched)                           // every launch's last waves (counters, work totals) first
+        for (DeviceState* ds : states) {
+            HIP_TRY(hipSetDevice(ds->device));
+            HIP_TRY(hipStreamWaitEvent(ds->stream, ds->fused_done, 0));
+        }
     if (whole) {   // every device's accumulation stream after its trace streams; the replicas' counters
         for (int k = 0; k < nsh; ++k) {
             DeviceState* ds = states[k];
@@ -1197,10 +1344,6 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
                 if (slots_used[k] & (1u << j)) HIP_TRY(hipStreamWaitEvent(ds->stream, ds->traced[j], 0));
         }
         if ((rc = merge_counters(sc, states, n, want_segs, want_draws))) return rc;
-    }
-    if (fused_launched) {                         // the launch's last waves (work totals) before the stats
-        HIP_TRY(hipSetDevice(h.device));
-        HIP_TRY(hipStreamWaitEvent(h.stream, h.fused_done, 0));
     }
     unsigned long long totals[kTotalSlots] = {};
     float kernel_ms = 0;
@@ -1264,8 +1407,13 @@ int rt_render(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progr
 }
 
 int rt_render_checkpoint(rt_scene* sc, double* sums, size_t count, int32_t* samples_done) {
-    if (!sc || !sums || !samples_done) return fail(RT_ERR_INVALID, "NULL argument");
+    if (!sc || !samples_done) return fail(RT_ERR_INVALID, "NULL argument");
     if (sc->ckpt_pixels == 0) return fail(RT_ERR_INVALID, "no render to checkpoint");
+    if (!sums && count == 0) {                     // samples_done only (the sums stay on the device)
+        *samples_done = sc->ckpt_done;
+        return RT_OK;
+    }
+    if (!sums) return fail(RT_ERR_INVALID, "NULL argument");
     if (count != 3 * sc->ckpt_pixels)
         return fail(RT_ERR_INVALID, "checkpoint holds %zu doubles, caller gave %zu", 3 * sc->ckpt_pixels, count);
     HIP_TRY(hipSetDevice(sc->home.device));
@@ -1277,9 +1425,17 @@ int rt_render_checkpoint(rt_scene* sc, double* sums, size_t count, int32_t* samp
 
 int rt_render_resume(rt_scene* sc, const rt_settings* s, const double* sums, int32_t samples_done,
                      const rt_output* out, rt_progress_fn progress, void* user, rt_stats* stats) {
-    if (!sums) return fail(RT_ERR_INVALID, "sums is NULL");
     if (s && (samples_done < std::max(0, s->sample_begin) || samples_done > s->samples))
         return fail(RT_ERR_INVALID, "samples_done %d outside [sample_begin, samples]", samples_done);
+    if (!sums) {                                   // from the scene's own checkpoint, still on its device
+        int cw = 0, ch = 0;
+        if (!sc) return fail(RT_ERR_INVALID, "scene is NULL");
+        if (int rc = check_settings(s, &cw, &ch)) return rc;
+        if (sc->ckpt_pixels == 0 || sc->ckpt_pixels != (size_t)cw * ch || samples_done != sc->ckpt_done)
+            return fail(RT_ERR_INVALID, "no resident checkpoint of %d samples over %d x %d pixels (sums NULL)",
+                        samples_done, cw, ch);
+        return render_impl(sc, s, out, progress, user, stats, nullptr, samples_done, true);
+    }
     return render_impl(sc, s, out, progress, user, stats, sums, samples_done);
 }
 
@@ -1302,6 +1458,10 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
     hipStream_t st = (hipStream_t)hip_stream;
     HIP_TRY(ds.total.ensure(kTotalSlots));
     ImageParams im = image_params(s, cw, ch);
+    if (use_pool(s)) {
+        im.tile_order = tile_order(sc, ds, im);
+        im.order_chunk0 = tile_order_mode() == 3 ? -1 : 0;
+    }
     Counters c{d_sum, nullptr, nullptr, ds.total.p};
     if (s->max_depth > 0 && (rc = ensure_partials(sc, ds, cw, ch, im.s_end - im.s_begin, use_pool(s), c))) return rc;
     HIP_TRY(order_scratch(ds, st));
@@ -1380,7 +1540,7 @@ int rt_finalize_device(rt_scene* sc, const rt_settings* s, const double* d_sum, 
     int rc = check_settings(s, &cw, &ch);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(sc->home.device));
-    HIP_TRY(epilogue(sc, s, cw, ch, d_sum, d_mean, d_post, d_rgba8, (hipStream_t)hip_stream));
+    HIP_TRY(epilogue(sc, s, cw, ch, d_sum, d_mean, d_post, d_rgba8, (hipStream_t)hip_stream, true));
     return RT_OK;
 }
 

@@ -31,6 +31,7 @@ struct HostScene {   // precision-independent staging, binary64 as packed by the
     int grid_n[3] = {0, 0, 0};
     float grid_lo[3] = {0, 0, 0}, grid_hi[3] = {0, 0, 0}, grid_cs[3] = {1, 1, 1}, grid_far = 0;
     bool use_grid = false;                                        // choose_walk(): the grid walks cheaper
+    std::vector<float> cost;                                      // estimate_costs(): kCostNX x kCostNY, top row first
     int bvh_depth = 0;                                            // deepest leaf of either tree
     int num_prims = 0;
     double record_bytes = 0;      // SURVEY §8d canonical bytes tested per segment
@@ -516,6 +517,31 @@ inline void build_bvhs(HostScene& hs) {
     hs.tri_wide = make_wide(hs.tri_bvh);
 }
 
+// The binary32 pre-filter record of a triangle {v0, e1, e2, ...} (binary64, pt_core.h tri_filter_bound):
+// the rounded vertex and edges and n = e2 x e1 (binary64 cross product, rounded); a triangle whose
+// |e1|inf or |e2|inf lies outside [2^-30, 2^30], or |v0|inf above 2^30, or with a non-finite coordinate,
+// gets n = NaN and is never rejected by the filter.
+inline TriFilter make_tri_filter(const double* t) {
+    TriFilter f;
+    double me1 = 0, me2 = 0, m0 = 0;
+    bool finite = true;
+    for (int k = 0; k < 3; ++k) {
+        f.v0[k] = (float)t[k];
+        f.e1[k] = (float)t[3 + k];
+        f.e2[k] = (float)t[6 + k];
+        m0 = std::max(m0, std::fabs(t[k]));
+        me1 = std::max(me1, std::fabs(t[3 + k]));
+        me2 = std::max(me2, std::fabs(t[6 + k]));
+        finite = finite && std::isfinite(t[k]) && std::isfinite(t[3 + k]) && std::isfinite(t[6 + k]);
+    }
+    const double* e1 = t + 3;
+    const double* e2 = t + 6;
+    const double n[3] = {e2[1] * e1[2] - e2[2] * e1[1], e2[2] * e1[0] - e2[0] * e1[2], e2[0] * e1[1] - e2[1] * e1[0]};
+    const bool ok = finite && m0 <= 0x1p30 && me1 >= 0x1p-30 && me1 <= 0x1p30 && me2 >= 0x1p-30 && me2 <= 0x1p30;
+    for (int k = 0; k < 3; ++k) f.n[k] = ok ? (float)n[k] : NAN;
+    return f;
+}
+
 // Record arrays of one precision (host memory); rt_capi.cpp uploads them, tests/hostcheck uses them.
 template <class R>
 struct HostRecords {
@@ -531,6 +557,7 @@ struct HostRecords {
     // triangles)
     std::vector<SphereLeaf<R>> bvh_sphere_leaf;
     std::vector<TriLeaf<R>> bvh_tri_leaf;
+    std::vector<TriFilter> tri_filter;            // binary64: bvh_tri_leaf's binary32 pre-filter records
     std::vector<SphereLeaf<R>> big_sphere_leaf;   // HostScene::big_spheres, tested before the walk
     std::vector<SphereLeaf<R>> grid_leaf;         // HostScene::grid_ids, cell by cell
 };
@@ -607,6 +634,7 @@ void make_records(const HostScene& hs, const rt_scene_desc& d, HostRecords<R>& o
         const TriRec<R>& r = out.tris[id];
         out.bvh_tri_leaf.push_back(TriLeaf<R>{{r.v0x, r.v0y, r.v0z, r.e1x, r.e1y, r.e1z, r.e2x, r.e2y, r.e2z},
                                               id, hs.tri_obj[id]});
+        if constexpr (sizeof(R) == 8) out.tri_filter.push_back(make_tri_filter(&hs.tris[12 * (size_t)id]));
     }
 }
 
@@ -667,10 +695,8 @@ inline uint32_t host_seed_mix(uint32_t seed) {
 #ifndef RT_GRID_CHOICE
 #define RT_GRID_CHOICE 0.8
 #endif
-inline void choose_walk(HostScene& hs, const rt_scene_desc& d) {
-    hs.use_grid = false;
-    if (hs.grid_n[0] * hs.grid_n[1] * hs.grid_n[2] <= 0 || !hs.tri_mat.empty() || hs.bvh_depth > 64) return;
-    HostRecords<double> rec;
+// A binary64 SceneView over host copies of the records (the host walks of choose_walk / estimate_costs)
+inline SceneView<double> host_view(const HostScene& hs, const rt_scene_desc& d, HostRecords<double>& rec) {
     make_records(hs, d, rec);
     SceneView<double> v{};
     v.runs = hs.runs.data();
@@ -682,10 +708,19 @@ inline void choose_walk(HostScene& hs, const rt_scene_desc& d) {
     v.plane_obj = hs.plane_obj.data(); v.box_obj = hs.box_obj.data();
     v.sphere_nodes = hs.sphere_bvh.data(); v.tri_nodes = hs.tri_bvh.data();
     v.bvh_sphere_leaf = rec.bvh_sphere_leaf.data(); v.bvh_tri_leaf = rec.bvh_tri_leaf.data();
+    v.tri_filter = rec.tri_filter.data();
     v.big_spheres = rec.big_sphere_leaf.data();
     v.sphere_wide = hs.sphere_wide.data(); v.tri_wide = hs.tri_wide.data();
     v.grid_cell = hs.grid_cell.data(); v.grid_leaf = rec.grid_leaf.data();
     fill_view_constants(v, hs, d);
+    return v;
+}
+
+inline void choose_walk(HostScene& hs, const rt_scene_desc& d) {
+    hs.use_grid = false;
+    if (hs.grid_n[0] * hs.grid_n[1] * hs.grid_n[2] <= 0 || !hs.tri_mat.empty() || hs.bvh_depth > 64) return;
+    HostRecords<double> rec;
+    const SceneView<double> v = host_view(hs, d, rec);
     const rt_camera_desc& c = d.camera;
     int stack[64];
     double tree = 0, grid = 0;
@@ -713,6 +748,45 @@ inline void choose_walk(HostScene& hs, const rt_scene_desc& d) {
     if (getenv("RT_WALK_DEBUG"))
         fprintf(stderr, "[rt] walk choice: tree %.3g, grid %.3g (%d x %d x %d cells) -> %s\n", tree, grid, hs.grid_n[0],
                 hs.grid_n[1], hs.grid_n[2], hs.use_grid ? "grid" : "tree");
+}
+
+// Estimated cost of the frame's regions (the pool's longest-first tile order, rt_capi.cpp tile_order): a
+// kCostNX x kCostNY raster of pixel-centre camera rays (no lens offset), each followed for up to three
+// segments (a random direction from every hit, as choose_walk) through the walk the trace kernel runs
+// (the kernel's own code on the host), costed as nodes or cells + 0.5 per sphere and 1.5 per triangle
+// test + 4 per segment (shading).  Only the order of the pool's items depends on it, never a result.
+constexpr int kCostNX = 96, kCostNY = 54;
+inline void estimate_costs(HostScene& hs, const rt_scene_desc& d) {
+    hs.cost.clear();
+    if (hs.bvh_depth > 64 || (hs.sphere_r.empty() && hs.tri_mat.empty())) return;
+    HostRecords<double> rec;
+    const SceneView<double> v = host_view(hs, d, rec);
+    const rt_camera_desc& c = d.camera;
+    int stack[64];
+    const BvhStack stk{stack, 1};
+    uint32_t rng = 0x2545F491u;
+    auto uni = [&]() { rng = rng * 1664525u + 1013904223u; return (double)(rng >> 8) * 0x1p-24 * 2.0 - 1.0; };
+    hs.cost.assign((size_t)kCostNX * kCostNY, 0.0f);
+    for (int row = 0; row < kCostNY; ++row)
+        for (int i = 0; i < kCostNX; ++i) {
+            const double u = (i + 0.5) / kCostNX, w = 1.0 - (row + 0.5) / kCostNY;
+            V3<double> o{c.origin[0], c.origin[1], c.origin[2]};
+            V3<double> dir{c.lower_left[0] + u * c.horizontal[0] + w * c.vertical[0] - o.x,
+                           c.lower_left[1] + u * c.horizontal[1] + w * c.vertical[1] - o.y,
+                           c.lower_left[2] + u * c.horizontal[2] + w * c.vertical[2] - o.z};
+            double cost = 0;
+            for (int seg = 0; seg < 3; ++seg) {
+                Work wk{};
+                const Closest<double> h = hs.use_grid ? closest_hit_grid<double>(v, o, dir, wk, stk)
+                                        : hs.tri_mat.empty() ? closest_hit_bvh<double, true, false>(v, o, dir, wk, stk)
+                                                             : closest_hit_bvh<double, true, true>(v, o, dir, wk, stk);
+                cost += wk.nodes + 0.5 * wk.spheres + 1.5 * wk.tris + 4.0;
+                if (h.kind == HIT_NONE) break;
+                o = o + dir * h.t;
+                dir = V3<double>{uni(), uni(), uni()};
+            }
+            hs.cost[(size_t)row * kCostNX + i] = (float)cost;
+        }
 }
 
 }  // namespace rt

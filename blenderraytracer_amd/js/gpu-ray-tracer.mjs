@@ -52,8 +52,11 @@ export function settingsOf(rt, opts = {}) {
         accel: ACCEL[opts.accel || 'auto'],
         // multi-GPU: every sample batch split over these HIP devices (rt_settings.devices)
         devices: opts.devices ? Array.from(opts.devices) : [],
-        // continue a cancelled render from its checkpoint ({sums, samplesDone}, rt_render_resume)
-        ...(opts.resume ? { resumeSums: opts.resume.sums, resumeSamplesDone: opts.resume.samplesDone } : {}),
+        // continue a cancelled render from its checkpoint (rt_render_resume): the sums still on the device
+        // (a lazy checkpointState nobody has read), or {sums, samplesDone} from the host
+        ...(opts.resume ? (opts.resume.resident
+            ? { resumeResident: 1, resumeSamplesDone: opts.resume.samplesDone }
+            : { resumeSums: opts.resume.sums, resumeSamplesDone: opts.resume.samplesDone }) : {}),
         cropX0: opts.crop ? opts.crop[0] : 0, cropY0: opts.crop ? opts.crop[1] : 0,
         cropW: opts.crop ? opts.crop[2] : 0, cropH: opts.crop ? opts.crop[3] : 0,
         wantMean: opts.wantMean ? 1 : 0, wantCounts: opts.wantCounts ? 1 : 0,
@@ -108,12 +111,37 @@ export function releaseGpuScene(rt) {
     if (rt.__gpuScene) { loadNative().destroyScene(rt.__gpuScene.scene); rt.__gpuScene = null; }
 }
 
+// The checkpoint of a cancelled render, lazily: samplesDone at once, the float64 sums (50 MB at 1080p)
+// copied from the device only when `.sums` is read — the cancel returns without that copy, and resume()
+// continues from the sums still on the device.  Valid until the RayTracer's next render (or a change of
+// its scene): read `.sums` before rendering again to keep it.
+function lazyCheckpoint(rt, nat, scene, samplesDone) {
+    const gen = rt.__renderGen;
+    let sums = null;
+    const live = () => gen === rt.__renderGen && rt.__gpuScene && rt.__gpuScene.scene === scene;
+    return {
+        samplesDone,
+        get resident() { return sums === null && live(); },
+        get sums() {
+            if (sums === null) {
+                if (!live()) throw new Error('checkpointState: superseded by a later render (read .sums before rendering again)');
+                sums = nat.checkpoint(scene).sums;
+            }
+            return sums;
+        },
+    };
+}
+
 // The GPU body of render(): trace, epilogue and readback; returns the native result (or null when
 // cancelled, like the reference which then stops silently, ray-tracer.js:256,264).
 export async function gpuRender(rt, onProgress, opts = {}) {
     const nat = loadNative();
     const scene = residentScene(rt, nat, opts.device || 0);
-    const st = settingsOf(rt, { preview: !!opts.intoImageData, ...opts });
+    // a resident checkpoint is resumed from the device (decided before this render supersedes it)
+    const resume = opts.resume && opts.resume.resident ? { resident: true, samplesDone: opts.resume.samplesDone }
+        : opts.resume ? { sums: opts.resume.sums, samplesDone: opts.resume.samplesDone } : undefined;
+    Object.defineProperty(rt, '__renderGen', { value: (rt.__renderGen || 0) + 1, writable: true, configurable: true, enumerable: false });
+    const st = settingsOf(rt, { preview: !!opts.intoImageData, ...opts, resume });
     // render() proper: the RGBA8 frame lands in this.imageData.data (full frame only), and with
     // st.preview every progress call first copies the running frame into it (the addon does that on
     // the main thread), so putImageData shows it like the reference's per-row repaint
@@ -133,7 +161,7 @@ export async function gpuRender(rt, onProgress, opts = {}) {
             // canvas: imageData holds the frame of the checkpointed samples; render({resume:
             // rt.checkpointState}) continues from them
             if (st.preview) repaint();
-            rt.checkpointState = nat.checkpoint(scene);
+            rt.checkpointState = lazyCheckpoint(rt, nat, scene, nat.checkpointSamples(scene));
             return null;
         }
         throw e;

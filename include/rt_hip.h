@@ -256,7 +256,11 @@ int rt_render(rt_scene* scene, const rt_settings* settings, const rt_output* out
  * of samples [sample_begin, samples_done).  rt_render_checkpoint copies them out (count must be
  * 3 x crop pixels) so a host can persist them; rt_render_resume traces samples
  * [samples_done, sample_end) on top of such sums and finishes like rt_render.  Every pixel still
- * adds its samples in order, so a resumed render is bit-identical to an uninterrupted one. */
+ * adds its samples in order, so a resumed render is bit-identical to an uninterrupted one.
+ * Resident checkpoints (no host copy of the sums): rt_render_checkpoint(scene, NULL, 0, &done)
+ * returns only samples_done, and rt_render_resume(..., sums = NULL, samples_done, ...) continues from
+ * the sums the scene still holds on its device — valid until the scene's next render (the call fails
+ * with RT_ERR_INVALID unless samples_done and the crop's pixel count are the checkpoint's). */
 int rt_render_checkpoint(rt_scene* scene, double* sums, size_t count, int32_t* samples_done);
 int rt_render_resume(rt_scene* scene, const rt_settings* settings, const double* sums, int32_t samples_done,
                      const rt_output* out, rt_progress_fn progress, void* user, rt_stats* stats);

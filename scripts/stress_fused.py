@@ -1,7 +1,9 @@
 """Fused-batch stress (DEV TOOL): many progressive renders with random batch sizes, previews and random
 cancels; every finished render must equal the same render in one batch up to the pool's summation
 order (SUM_RTOL), every cancelled one must leave a checkpoint that resumes to the uninterrupted sums
-bit for bit.  usage: python scripts/stress_fused.py [renders]"""
+bit for bit.  A third of the renders deal their batches to devices=[0, 0] or [0, 0, 0] (the whole-batch
+split, one fused launch per device since round 5; bit-identical to one device).
+usage: python scripts/stress_fused.py [renders]"""
 import os
 import random
 import sys
@@ -27,10 +29,20 @@ for i in range(n):
     assert rt.load_from_json(scenes[name])
     rt.update_render_settings({"samples": spp, "maxBounces": 5})
     ref = rt.render(want=("mean",), batch_samples=batch)["mean"]          # fused (or not) progressive
+    devices = rnd.choice([None, None, [0, 0], [0, 0, 0]])
+    if devices:
+        # the whole-batch split deals batches of min(batch, ceil(spp / N)) samples (rt_capi.cpp): the same
+        # sums bit for bit as those batches on one device
+        batch = min(batch, -(-spp // len(devices)))
+        ref = rt.render(want=("mean",), batch_samples=batch)["mean"]
+        split = rt.render(want=("mean",), batch_samples=batch, devices=devices)["mean"]
+        if not np.array_equal(split, ref, equal_nan=True):
+            bad += 1
+            print(f"render {i}: {name} {w}x{h} spp {spp} batch {batch} devices {devices}: split != one device", flush=True)
     calls = []
     stop_at = rnd.randint(1, max(1, spp // batch))
     try:
-        rt.render(want=("mean", "preview"), batch_samples=batch,
+        rt.render(want=("mean", "preview"), batch_samples=batch, devices=devices,
                   on_progress=lambda f: calls.append(f) or len(calls) >= stop_at)
         cancelled = False
     except RuntimeError as e:
@@ -39,7 +51,7 @@ for i in range(n):
             raise
     if cancelled:
         sums, done = rt.checkpoint()
-        res = rt.render(want=("mean",), batch_samples=batch, resume=(sums, done))["mean"]
+        res = rt.render(want=("mean",), batch_samples=batch, resume=(sums, done), devices=devices)["mean"]
         ok = np.array_equal(res, ref, equal_nan=True)
     else:
         ok = True

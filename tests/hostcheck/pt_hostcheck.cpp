@@ -30,6 +30,7 @@ struct HostView {
         v.plane_obj = hs.plane_obj.data(); v.box_obj = hs.box_obj.data();
         v.sphere_nodes = hs.sphere_bvh.data(); v.tri_nodes = hs.tri_bvh.data();
         v.bvh_sphere_leaf = rec.bvh_sphere_leaf.data(); v.bvh_tri_leaf = rec.bvh_tri_leaf.data();
+        v.tri_filter = rec.tri_filter.data();
         v.big_spheres = rec.big_sphere_leaf.data();
         v.sphere_wide = hs.sphere_wide.data(); v.tri_wide = hs.tri_wide.data();
         v.grid_cell = hs.grid_cell.data(); v.grid_leaf = rec.grid_leaf.data();
@@ -383,4 +384,100 @@ extern "C" void ptc_root_div(const double* x, const double* a, double* out, long
 }
 extern "C" void ptc_root_div_f32(const float* x, const float* a, float* out, long long n) {
     for (long long i = 0; i < n; ++i) out[i] = rt::root_div<float>(x[i], a[i], rt::root_rcp<float>(a[i]));
+}
+
+// vdiv_rcp's scalar division (pt_core.h div_rcp_1, TEST TOOL).  Binary32: every significand of x in
+// [1, 2) against `ndiv` divisors (the 64 largest significands, all ones first, then random ones); returns
+// the mismatches against the IEEE division.  Binary64: out2 = div_rcp_1 (two corrections), out1 = the
+// single correction of round 4 (for the record) of given pairs (tests/test_root_div.py builds hard cases).
+static float f32_bits(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+extern "C" long long ptc_div_rcp_f32_exhaustive(int ndiv, unsigned seed) {
+    std::mt19937 gen(seed);
+    long long bad = 0;
+    for (int ib = 0; ib < ndiv; ++ib) {
+        const uint32_t bm = ib < 64 ? 0x7FFFFFu - (uint32_t)ib : (uint32_t)(gen() >> 9);
+        const float s = f32_bits(0x3F800000u | bm), y = 1.0f / s;
+        for (uint32_t am = 0; am < (1u << 23); ++am) {
+            const float x = f32_bits(0x3F800000u | am);
+            bad += rt::div_rcp_1<float>(x, s, y) != x / s;
+        }
+    }
+    return bad;
+}
+extern "C" void ptc_div_rcp_f64(const double* x, const double* s, double* out2, double* out1, long long n) {
+    for (long long i = 0; i < n; ++i) {
+        const double y = 1.0 / s[i], q0 = x[i] * y;
+        out2[i] = rt::div_rcp_1<double>(x[i], s[i], y);
+        out1[i] = std::fma(std::fma(-q0, s[i], x[i]), y, q0);
+    }
+}
+
+// Adversarial check of the binary32 triangle pre-filter (pt_core.h tri_filter_pass, tri_filter_bound):
+// random triangles over 7 decades of scale and shape (slivers included), rays through points at
+// barycentric distance 10^-1 .. 10^-12 from an edge or a vertex (inside and outside), rays whose A = d.n
+// sits at the 1e-4 threshold, origins at t = 0.001 (1 +- eps) before the plane, and a best hit at the
+// triangle's t (1 +- eps).  Returns the number of cases the filter rejected although the binary64 test
+// (triangle_candidate + `better`) accepts (must be 0); *reject_frac: the fraction of the binary64
+// rejections the filter also rejects; *pass_frac: the fraction of all cases it lets through.
+extern "C" long long ptc_tri_filter_check(long long n, unsigned seed, double* reject_frac, double* pass_frac) {
+    std::mt19937_64 gen(seed);
+    std::uniform_real_distribution<double> U(-1.0, 1.0);
+    long long bad = 0, rej64 = 0, rej_both = 0, passed = 0;
+    for (long long it = 0; it < n; ++it) {
+        const double scale = std::pow(10.0, 3.5 * U(gen));
+        const double size = scale * std::pow(10.0, -3.0 * std::fabs(U(gen)));   // triangle size vs position
+        double t9[12];
+        for (int k = 0; k < 3; ++k) t9[k] = U(gen) * scale;
+        double e1[3], e2[3];
+        for (int k = 0; k < 3; ++k) { e1[k] = U(gen) * size; e2[k] = U(gen) * size; }
+        if (it % 7 == 0) for (int k = 0; k < 3; ++k) e2[k] = e1[k] * (1 + 1e-3 * U(gen)) + 1e-6 * size * U(gen);   // sliver
+        for (int k = 0; k < 3; ++k) { t9[3 + k] = (t9[k] + e1[k]) - t9[k]; t9[6 + k] = (t9[k] + e2[k]) - t9[k]; }
+        // target: barycentric (bu, bv) near an edge / vertex / inside
+        const int mode = (int)(gen() % 5);
+        const double eps = std::pow(10.0, -11.0 * std::fabs(U(gen)) - 1.0) * (U(gen) < 0 ? -1 : 1);
+        double bu = std::fabs(U(gen)), bv = std::fabs(U(gen));
+        if (bu + bv > 1) { bu = 1 - bu; bv = 1 - bv; }
+        if (mode == 0) bu = eps;                      // edge u = 0
+        else if (mode == 1) bv = eps;                 // edge v = 0
+        else if (mode == 2) bv = 1 - bu + eps;        // edge u + v = 1
+        else if (mode == 3) { bu = 1 + eps; bv = 0; } // vertex v1
+        double P[3];
+        for (int k = 0; k < 3; ++k) P[k] = t9[k] + bu * t9[3 + k] + bv * t9[6 + k];
+        // direction: random, or grazing (|d.n| ~ 1e-4 threshold), of length 10^-2 .. 10^2
+        double dd[3] = {U(gen), U(gen), U(gen)};
+        const double nn[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+        const double nl = std::sqrt(nn[0] * nn[0] + nn[1] * nn[1] + nn[2] * nn[2]);
+        const double dl = std::pow(10.0, 2.0 * U(gen));
+        if (it % 3 == 1 && nl > 0) {
+            // d = in-plane part + the normal component that puts |A| at 1e-4 (1 + eps2)
+            const double dn = (dd[0] * nn[0] + dd[1] * nn[1] + dd[2] * nn[2]) / (nl * nl);
+            for (int k = 0; k < 3; ++k) dd[k] -= dn * nn[k];
+            const double want = 1e-4 * (1 + std::pow(10.0, -10.0 * std::fabs(U(gen)) - 2.0) * (U(gen) < 0 ? -1 : 1));
+            for (int k = 0; k < 3; ++k) dd[k] = dd[k] * dl + (U(gen) < 0 ? -1 : 1) * want * nn[k] / (nl * nl);
+        } else {
+            for (int k = 0; k < 3; ++k) dd[k] *= dl;
+        }
+        // origin: back along d by tb (tb = 0.001 (1 + eps) some of the time: the tmin edge)
+        const double tb = it % 4 == 2 ? 0.001 * (1 + std::pow(10.0, -10.0 * std::fabs(U(gen)) - 2.0) * (U(gen) < 0 ? -1 : 1))
+                                      : std::pow(10.0, 3.0 * U(gen));
+        double o[3];
+        for (int k = 0; k < 3; ++k) o[k] = P[k] - dd[k] * tb;
+        TriRec<double> tr{t9[0], t9[1], t9[2], t9[3], t9[4], t9[5], t9[6], t9[7], t9[8], 0, 0, 0};
+        const V3<double> O{o[0], o[1], o[2]}, D{dd[0], dd[1], dd[2]};
+        double t = 0;
+        const bool cand = triangle_candidate(tr, O, D, 0.001, t);
+        // the current best: none, or at the triangle's t (1 + eps), ties won by this triangle
+        Closest<double> b{INFINITY, HIT_NONE, 0, 0, 1 << 30};
+        if (it & 1) b.t = (cand ? t : tb) * (1 + std::pow(10.0, -12.0 * std::fabs(U(gen)) - 1.0) * (U(gen) < 0 ? -1 : 1));
+        if (it % 16 == 5 && cand) b.t = t;             // exact tie
+        const bool accept = cand && better(t, 0, 0, b);
+        const TriFilter f = make_tri_filter(t9);
+        const bool pass = tri_filter_pass(f, make_tri_ray(O, D), bvh_tlimit(b.t));
+        if (accept && !pass) ++bad;
+        if (!accept) { ++rej64; rej_both += !pass; }
+        passed += pass;
+    }
+    *reject_frac = rej64 ? (double)rej_both / rej64 : 0;
+    *pass_frac = n ? (double)passed / n : 0;
+    return bad;
 }

@@ -79,10 +79,36 @@ if (cmd === 'pack') {
         let calls = 0;
         await part.render(() => { if (++calls === 2) global.window.renderCancelled = true; });
         const done = part.checkpointState ? part.checkpointState.samplesDone : -1;
+        const resident = !!(part.checkpointState && part.checkpointState.resident);
         global.window.renderCancelled = false;
-        await part.resume();
+        await part.resume();                                   // from the sums still on the device
         const a = full.imageData.data, b = part.imageData.data;
-        summary._resume = { samplesDone: done, equal: a.length === b.length && a.every((v, i) => v === b[i]) };
+        // the same with the checkpoint's sums read to the host first (persisted and handed back)
+        const { rt: host } = tracerFor('kitchen_sink', { batchSamples: 2 });
+        host.updateRenderSettings({ samples: 16 });
+        calls = 0;
+        global.window.renderCancelled = false;
+        await host.render(() => { if (++calls === 2) global.window.renderCancelled = true; });
+        global.window.renderCancelled = false;
+        const saved = { sums: Float64Array.from(host.checkpointState.sums), samplesDone: host.checkpointState.samplesDone };
+        const hostResident = host.checkpointState.resident;
+        host.checkpointState = saved;
+        await host.resume();
+        const c = host.imageData.data;
+        // a checkpoint nobody read is superseded by the next render
+        const { rt: stale } = tracerFor('kitchen_sink', { batchSamples: 2 });
+        stale.updateRenderSettings({ samples: 16 });
+        calls = 0;
+        await stale.render(() => { if (++calls === 2) global.window.renderCancelled = true; });
+        global.window.renderCancelled = false;
+        const old = stale.checkpointState;
+        await stale.render();
+        let superseded = false;
+        try { void old.sums; } catch (e) { superseded = /superseded/.test(String(e)); }
+        summary._resume = {
+            samplesDone: done, resident, equal: a.length === b.length && a.every((v, i) => v === b[i]),
+            hostResident, hostEqual: a.every((v, i) => v === c[i]), superseded,
+        };
     }
     // progressive display (ray-tracer.js:224-264): render() splits the samples into 16 batches, and at
     // every progress call imageData already holds the frame of the samples done so far; a cancel

@@ -827,10 +827,9 @@ def test_progressive_preview_and_cancel(gpu):
     res = rt.render(want=("preview",), batch_samples=2, on_progress=lambda f: fr.append(f) and False)
     assert len(fr) >= 16 and all(x < y for x, y in zip(fr, fr[1:])) and fr[-1] == 1.0
     rt30 = _rtow(128, 72, 30, seed=6)
-    # running frames come from preview_kernel, whose gamma pow is binary32 (pt_trace.hip): within one
-    # RGBA8 step of the exact frame, on pixels within ~1e-7 of a rounding boundary
-    d = np.abs(res["preview"].astype(np.int32) - rt30.render(batch_samples=2)["rgba8"].astype(np.int32))
-    assert d.max() <= 1 and np.count_nonzero(d) <= 1e-3 * d.size, (d.max(), np.count_nonzero(d))
+    # running frames come from preview_kernel (gamma thresholds instead of a binary64 pow, pt_trace.hip):
+    # the same bytes as the exact epilogue
+    assert np.array_equal(res["preview"], rt30.render(batch_samples=2)["rgba8"])
     assert not np.array_equal(res["preview"], res["rgba8"])
     rt30.close()
     calls = []
@@ -883,3 +882,43 @@ def test_overlapped_batches_equal_serial_batches(gpu, tmp_path):
         ref = serial["rtow.json.5.None"] if k == two else serial[k]
         assert np.array_equal(over[k], ref, equal_nan=True), k
         assert np.array_equal(unfused[k], ref, equal_nan=True), k
+
+
+@pytest.mark.parametrize("gamma", [2.2, 1.0, 0.45, 3.7])
+def test_preview_thresholds_match_finalize(gpu, gamma):
+    """preview_kernel's RGBA8 bytes (the count of gamma thresholds T_k <= tm, T_k computed with the
+    device's own binary64 pow) against finalize_kernel's floor(255 pow(max(0, tm), 1/gamma)) on tone-mapped
+    values within +-3000 ulps of every threshold (where a non-monotone pow or an off-by-one search would
+    show), plus random, negative, zero, huge, infinite and NaN values: rt_finalize_device with RGBA8 only
+    takes the threshold kernel, with the Float32 frame requested too finalize_kernel (linear tone map,
+    exposure 1, one sample: tm = the sum)."""
+    import torch
+    k = np.arange(1, 256, dtype=np.float64)
+    approx = (k / 255.0) ** gamma                                  # T_k up to a few ulps
+    steps = np.arange(-3000, 3001, dtype=np.int64)
+    near = (approx.view(np.int64)[:, None] + steps[None, :]).ravel().view(np.float64)
+    rng = np.random.default_rng(2)
+    extra = np.concatenate([rng.uniform(-0.5, 1.5, 200_000), 10.0 ** rng.uniform(-30, 30, 100_000),
+                            [0.0, -0.0, -1.0, 1.0, np.inf, -np.inf, np.nan, 5e-324, 1e300]])
+    tm = np.concatenate([near, extra])
+    n = -(-tm.size // 3)
+    tm = np.concatenate([tm, np.zeros(3 * n - tm.size)])
+    lib = capi.load_library()
+    rt = _rtow(n, 1, 1, seed=1)
+    rt.tone_mapping, rt.exposure, rt.gamma = "linear", 1.0, gamma
+    scene = rt.scene_handle()
+    st = rt.settings()
+    d_sum = torch.from_numpy(tm).cuda()
+    fast = torch.zeros(4 * n, dtype=torch.uint8, device="cuda")
+    exact = torch.zeros(4 * n, dtype=torch.uint8, device="cuda")
+    post = torch.zeros(4 * n, dtype=torch.float32, device="cuda")
+    capi.check(lib.rt_finalize_device(scene, C.byref(st), C.c_void_p(d_sum.data_ptr()), None, None,
+                                      C.c_void_p(fast.data_ptr()), None))
+    capi.check(lib.rt_finalize_device(scene, C.byref(st), C.c_void_p(d_sum.data_ptr()), None,
+                                      C.c_void_p(post.data_ptr()), C.c_void_p(exact.data_ptr()), None))
+    torch.cuda.synchronize()
+    f, e = fast.cpu().numpy(), exact.cpu().numpy()
+    assert np.array_equal(f, e), int(np.count_nonzero(f != e))
+    assert len(np.unique(e)) == 256                                 # every byte value was exercised
+    rt.close()
+

@@ -160,8 +160,11 @@ def test_js_gpu_render_matches_reference(gpu):
         # before the render goes on): the batches queued stop at their next item, the checkpoint holds
         # the batches reduced before that (2 to 5 of them), then GpuRayTracer.resume(): the same image as
         # the uninterrupted render
-        assert summary["_resume"]["equal"] is True
-        assert summary["_resume"]["samplesDone"] in (4, 6, 8, 10), summary["_resume"]
+        rs = summary["_resume"]
+        assert rs["equal"] is True and rs["resident"] is True, rs    # resumed from the device-resident sums
+        assert rs["hostEqual"] is True and rs["hostResident"] is False, rs   # from sums read to the host
+        assert rs["superseded"] is True, rs
+        assert rs["samplesDone"] in (4, 6, 8, 10), rs
         dv = summary["_devices"]                    # settings.devices = [0, 0] through N-API
         assert dv["segsEqual"] and dv["drawsEqual"] and dv["maxRel"] <= 1e-13, dv
         assert dv["sceneCached"] and dv["reuploaded"], dv

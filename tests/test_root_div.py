@@ -56,3 +56,53 @@ def test_root_div_equals_division_binary32():
         ref = x / a
     got = _root_div(x, a, np.float32)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), int(np.count_nonzero(got != ref))
+
+
+def _hard_f64_pairs(n, seed):
+    """Binary64 (x, s) whose quotient lies within a few 2^-105 of a midpoint between two binary64 numbers
+    (or of a binary64 number): with integer significands X, S in [2^52, 2^53), X 2^53 - S Q = N for a small
+    N, so x / s = (Q + N / S) 2^-53 — the cases a division through a reciprocal can round the wrong way."""
+    rng = np.random.default_rng(seed)
+    xs, ss = [], []
+    two53 = 1 << 53
+    while len(xs) < n:
+        S = int(rng.integers(1 << 52, 1 << 53)) | 1
+        N = int(rng.choice([-3, -2, -1, 1, 2, 3]))
+        X = (N * pow(two53, -1, S)) % S
+        while X < (1 << 52):
+            X += S
+        if X >= two53:
+            continue
+        assert (X * two53 - N) % S == 0
+        e = int(rng.integers(-60, 60))
+        xs.append(np.ldexp(float(X), e - 52) * (1 if rng.random() < 0.5 else -1))
+        ss.append(np.ldexp(float(S), int(rng.integers(-60, 60)) - 52))
+    return np.array(xs), np.array(ss)
+
+
+def test_vdiv_rcp_f64_hard_cases():
+    """vdiv_rcp's binary64 division (two Markstein corrections) on near-midpoint quotients and random
+    pairs: bit-identical to the IEEE division.  The single correction of round 4 is reported, not used."""
+    L = hc.lib()
+    L.ptc_div_rcp_f64.argtypes = [C.POINTER(C.c_double)] * 4 + [C.c_longlong]
+    xh, sh = _hard_f64_pairs(60_000, 3)
+    rng = np.random.default_rng(5)
+    xr = rng.normal(0, 1, 200_000) * np.exp2(rng.uniform(-400, 400, 200_000))
+    sr = rng.uniform(0.5, 2, 200_000) * np.exp2(rng.uniform(-300, 300, 200_000))
+    x, s = np.concatenate([xh, xr]), np.concatenate([sh, sr])
+    out2, out1 = np.empty_like(x), np.empty_like(x)
+    p = lambda v: v.ctypes.data_as(C.POINTER(C.c_double))   # noqa: E731
+    L.ptc_div_rcp_f64(p(x), p(s), p(out2), p(out1), len(x))
+    ref = x / s
+    assert np.array_equal(out2.view(np.uint64), ref.view(np.uint64)), int(np.count_nonzero(out2 != ref))
+    print(f"single correction: {int(np.count_nonzero(out1 != ref))} of {len(x)} differ "
+          f"({int(np.count_nonzero(out1[:len(xh)] != ref[:len(xh)]))} of {len(xh)} hard cases)")
+
+
+def test_vdiv_rcp_f32_every_significand():
+    """vdiv_rcp's binary32 division (one Markstein correction): every significand of x against 64
+    all-ones-adjacent and 16 random divisor significands (671 M divisions), bit-identical to IEEE."""
+    L = hc.lib()
+    L.ptc_div_rcp_f32_exhaustive.argtypes = [C.c_int, C.c_uint]
+    L.ptc_div_rcp_f32_exhaustive.restype = C.c_longlong
+    assert L.ptc_div_rcp_f32_exhaustive(80, 99) == 0
