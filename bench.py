@@ -190,6 +190,7 @@ FLOOR_COST = {
     "f64_sphere_tests": 36,     # oc, halfB, c, discriminant: 17 binary64 ops + compare (geometry.js:16-22)
     "disc_nonneg": 58,          # sqrt + (-halfB - sqrtd) / a + tMin test (geometry.js:24-26)
     "second_root": 26,          # (-halfB + sqrtd) / a + test (geometry.js:27-28)
+    "tri_filter_tests": 52,     # binary32 triangle pre-filter: 21 FMA-chain ops + bounds + 6 tests (pt_core.h)
     "tri_tests": 102,           # Moller-Trumbore: 2 cross, 4 dot, 1 division (geometry.js:148-188)
     "plane_tests": 50,          # dot, (p - o).n / denom (geometry.js:56-74)
     "box_tests": 150,           # six divisions + slab logic (geometry.js:85-117)

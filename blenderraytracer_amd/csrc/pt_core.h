@@ -99,8 +99,11 @@ template <class R> RT_HD V3<R> cross(V3<R> a, V3<R> b) {
 #ifndef RT_DIV_F64_TWICE
 #define RT_DIV_F64_TWICE 1        // 0 (A/B): round 4's single correction in binary64 too
 #endif
+// Binary64 measured (RTOW 256 spp f64, interleaved x2): two corrections 10197, IEEE divisions 10260, round
+// 4's single correction 10299 Msamples/s — so binary64 takes the IEEE divisions (RT_DIV_RCP_F64 = 0:
+// exact by definition; 1: the provable two-correction form above, A/B)
 #ifndef RT_DIV_RCP_F64
-#define RT_DIV_RCP_F64 1          // 0 (A/B): binary64 vectors through the IEEE divisions
+#define RT_DIV_RCP_F64 0
 #endif
 template <class R> constexpr bool div_rcp_on() { return RT_DIV_RCP && (sizeof(R) == 4 || RT_DIV_RCP_F64); }
 template <class R> RT_HD R div_rcp_1(R x, R s, R y) {           // guarded by the caller
@@ -140,6 +143,15 @@ template <class R> struct SphereRec { R cx, cy, cz, r2; };            // r2 = ra
 // binary32 pre-filter record of a sphere (f64 mode only): centre rounded to f32 and the radius^2
 // inflated by the error bound, r2p = r^2 + 2^-17 (2|c|^2 + r^2), rounded up; see sphere_filter_bound.
 struct SphereFilter { float cx, cy, cz, r2p; };
+// the filter's margin 2^RT_FILTER_MARGIN Q (sphere_filter_bound)
+#ifndef RT_FILTER_MARGIN
+#define RT_FILTER_MARGIN (-17)
+#endif
+constexpr double filter_margin() {   // 2^RT_FILTER_MARGIN, exact
+    double v = 1.0;
+    for (int k = 0; k > RT_FILTER_MARGIN; --k) v *= 0.5;
+    return v;
+}
 template <class R> struct PlaneRec { R px, py, pz, nx, ny, nz; };
 template <class R> struct BoxRec { R mnx, mny, mnz, mxx, mxy, mxz; };
 template <class R> struct TriRec { R v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z, nx, ny, nz; };  // e1=v1-v0, e2=v2-v0
@@ -267,11 +279,16 @@ RT_HD void sphere_test_f64(const SceneView<R>& sc, V3<R> o, V3<R> d, R a, R tmin
 // The filter evaluates X = (oc32.dn)^2 - |oc32|^2 + r2p + delta in binary32 (u = 2^-24) from rounded
 // o, c and the normalized rounded direction dn, with r2p = r^2 + 2^-17 (2|c|^2 + r^2) and
 // delta = 2^-16 |o|^2 (both rounded up).  With M_i = |o_i| + |c_i| and Q = sum M_i^2 + r^2 <=
-// 2|o|^2 + 2|c|^2 + r^2, the rounding terms are |(oc32.dn)^2 - (OC.n)^2| <= 18u Q (oc error 2u M,
-// direction error 4u, dot 3u), ||oc32|^2 - |OC|^2| <= 7u Q and <= 2u Q for the final roundings:
-// |X - Y - (r2p - r^2) - delta| <= 27u Q, while r2p - r^2 + delta >= 2^-17 Q = 128u Q.  Hence
-// disc64 >= 0 (Y >= -2^-48 Q) implies X > 0: a rejected sphere (X < 0) is a sure binary64 miss.
-// NaN never rejects.  tests/test_sphere_filter.py checks this on adversarial near-tangent cases.
+// 2|o|^2 + 2|c|^2 + r^2: oc32 is within 2u M_i of OC per component; dn within 6.5u of n (d rounded u,
+// the sum of squares 2.5u, v_rsq_f32 2u, the product u); so the three-term dot oc32.dn is within
+// (2 + 6.5 + 3)u |M| of OC.n (3u: the FMA chain's roundings) and |(oc32.dn)^2 - (OC.n)^2| <= 23u Q;
+// ||oc32|^2 - |OC|^2| <= 4u Q and the chain that subtracts r2p + delta rounds by <= 6u Q; the final
+// FMA's rounding cannot change the sign of X.  So |X - Y - (r2p - r^2) - delta| <= 33u Q, while
+// r2p - r^2 + delta >= 2^-17 Q = 128u Q (3.9x margin; 2^-18 .. 2^-20 cut the binary64 tests per RTOW
+// segment by 0.3 % at most, host count: most filter survivors are real hits, or the dominant spheres'
+// away-rejections).  Hence disc64 >= 0 (Y >= -2^-48 Q) implies X > 0: a rejected
+// sphere (X < 0) is a sure binary64 miss.  NaN never rejects.  tests/test_sphere_filter.py checks this on
+// adversarial near-tangent cases (observed worst 7.4u with a correctly rounded rsqrt).
 // Approximate binary32 reciprocal / reciprocal square root (v_rcp_f32 / v_rsq_f32, <= 1 ulp) for the
 // conservative binary32 pre-tests only (sphere filter direction, BVH slab 1/d): their error bounds
 // (sphere_filter_bound, bvh_conservative_bound) carry margins of 4x and 16x over a correctly rounded
@@ -304,7 +321,7 @@ RT_HD FilterRay make_filter_ray(V3<R> o, V3<R> d) {
     const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
     const float inv = rt_rsqrt_approx(dx * dx + dy * dy + dz * dz);
     f.dx = dx * inv; f.dy = dy * inv; f.dz = dz * inv;
-    f.delta = (f.ox * f.ox + f.oy * f.oy + f.oz * f.oz) * (0x1p-16f * (1.0f + 0x1p-20f));
+    f.delta = (f.ox * f.ox + f.oy * f.oy + f.oz * f.oz) * ((float)(2.0 * filter_margin()) * (1.0f + 0x1p-20f));
     return f;
 }
 

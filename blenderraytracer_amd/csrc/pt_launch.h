@@ -112,10 +112,21 @@ struct FinalizeParams {
 // thresholds: a running frame of a progressive render (RGBA8 only) through preview_kernel, whose bytes
 // come from the 255 gamma thresholds of launch_gamma_thresholds instead of a binary64 pow (the same
 // bytes as finalize_kernel in 29 VGPRs, so it runs beside the trace waves; pt_trace.hip)
+// The RGBA8 bytes of a gamma as a step function of the tone-mapped value (pt_trace.hip preview_kernel):
+// t[k - 1] = the least binary64 tm whose byte is >= k, plus the values near the thresholds where the
+// device pow is not monotone (exceptions: tm and its byte), found by scanning +-kGammaScan ulps of every
+// threshold; overflow: more exceptions than kGammaExc (the table is then not used)
+constexpr int kGammaExc = 1024, kGammaScan = 4096;
+struct GammaTable {
+    double t[255];
+    uint32_t n_exc, overflow;
+    double exc_tm[kGammaExc];
+    uint32_t exc_byte[kGammaExc];
+};
 hipError_t launch_finalize(const FinalizeParams& p, const double* sum, double* mean, float* post, uint8_t* rgba8,
-                           hipStream_t stream, const double* thresholds = nullptr);
+                           hipStream_t stream, const GammaTable* thresholds = nullptr);
 bool preview_thresholds_ok(double gamma);
-hipError_t launch_gamma_thresholds(double gamma, double* T, hipStream_t stream);
+hipError_t launch_gamma_thresholds(double gamma, GammaTable* T, hipStream_t stream);
 hipError_t launch_denoise(int w, int h, double w1, double w2, const float* in, float* out, uint8_t* rgba8,
                           hipStream_t stream);
 

@@ -1137,17 +1137,31 @@ __global__ __launch_bounds__(64) void finalize_kernel(const FinalizeParams p, co
 // for trace waves to exit (measured 0.2 - 7.5 ms per preview, delaying the next batches' reduces on the
 // same stream; a fused launch's waves never exit).  The binary64 pow alone needs 64 VGPRs, so the
 // preview does without it: the byte finalize_kernel stores, floor(255 pow(max(0, tm), 1/gamma)) clamped,
-// is a non-decreasing step function of the tone-mapped value tm, so it equals the number of thresholds
-// T_k <= tm, T_k (k = 1..255) the least binary64 tm whose byte is >= k — computed once per gamma by
-// gamma_thresholds_kernel with the device's own binary64 pow (finalize_kernel's).  The preview computes
-// tm exactly as finalize_kernel (binary64, same operations) and counts the thresholds by binary search:
-// the same bytes (tests/test_gpu_parity.py::test_progressive_preview_and_cancel, and the threshold
-// neighbourhoods in ::test_preview_thresholds_match_finalize).  NaN tm: byte 0, as to_u8.
+// is a step function of the tone-mapped value tm, non-decreasing wherever the device pow is monotone, so
+// it equals the number of thresholds T_k <= tm, T_k (k = 1..255) the least binary64 tm whose byte is >= k
+// (a binary search over the binary64 bit patterns with the device's own pow, gamma_thresholds_kernel).
+// Where the pow is not monotone — measured: 1 value in the +-3000 ulps around the thresholds of gamma 2.2
+// — the count is wrong, and such values can only lie next to a threshold (a pow error of an ulp moves the
+// byte only where 255 pow(tm) is within ulps of an integer): gamma_exceptions_kernel evaluates the byte on
+// the +-kGammaScan ulps around every threshold and records every value whose byte differs from the count;
+// the preview checks those exceptions (none or a few).  The preview computes tm exactly as
+// finalize_kernel (binary64, same operations): the same bytes (tests/test_gpu_parity.py::
+// test_progressive_preview_and_cancel, ::test_preview_thresholds_match_finalize).  NaN tm: byte 0, as to_u8.
 __device__ __forceinline__ uint32_t gamma_byte(double tm, double inv_gamma) {
     return to_u8(pow(js_max<double>(0.0, tm), inv_gamma));
 }
-__global__ __launch_bounds__(256) void gamma_thresholds_kernel(const double inv_gamma, double* __restrict__ T) {
+__device__ __forceinline__ uint32_t gamma_count(const double* __restrict__ t, double tm) {
+    uint32_t lo = 0, n = 255;            // the number of thresholds <= tm (t ascending; a NaN tm passes none)
+    while (n > 0) {
+        const uint32_t h = n >> 1;
+        if (t[lo + h] <= tm) { lo += h + 1; n -= h + 1; }
+        else n = h;
+    }
+    return lo;
+}
+__global__ __launch_bounds__(256) void gamma_thresholds_kernel(const double inv_gamma, GammaTable* __restrict__ g) {
     const uint32_t k = threadIdx.x + 1;
+    if (threadIdx.x == 0) { g->n_exc = 0; g->overflow = 0; }
     if (k > 255) return;
     // smallest non-negative binary64 tm (by bit pattern, the same order) with byte(tm) >= k:
     // byte(+0) = 0 < k, byte(+inf) = 255 >= k
@@ -1157,13 +1171,28 @@ __global__ __launch_bounds__(256) void gamma_thresholds_kernel(const double inv_
         if (gamma_byte(__longlong_as_double((long long)mid), inv_gamma) >= k) hi = mid;
         else lo = mid;
     }
-    T[k - 1] = __longlong_as_double((long long)hi);
+    g->t[k - 1] = __longlong_as_double((long long)hi);
+}
+// block k - 1 scans +-kGammaScan ulps around threshold k (32 values per thread)
+__global__ __launch_bounds__(256) void gamma_exceptions_kernel(const double inv_gamma, GammaTable* __restrict__ g) {
+    const int64_t center = __double_as_longlong(g->t[blockIdx.x]);
+    for (int j = 0; j < 2 * kGammaScan / 256; ++j) {
+        const int64_t bits = center - kGammaScan + (int64_t)threadIdx.x * (2 * kGammaScan / 256) + j;
+        if (bits < 0 || bits >= (int64_t)0x7FF0000000000000ll) continue;
+        const double tm = __longlong_as_double(bits);
+        const uint32_t b = gamma_byte(tm, inv_gamma);
+        if (b == gamma_count(g->t, tm)) continue;
+        const uint32_t e = atomicAdd(&g->n_exc, 1u);
+        if (e < (uint32_t)kGammaExc) { g->exc_tm[e] = tm; g->exc_byte[e] = b; }
+        else g->overflow = 1;
+    }
 }
 
 __global__ __launch_bounds__(64) void preview_kernel(const FinalizeParams p, const double* __restrict__ sum,
-                                                     const double* __restrict__ T, uint8_t* __restrict__ rgba8) {
+                                                     const GammaTable* __restrict__ g, uint8_t* __restrict__ rgba8) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= p.n) return;
+    const uint32_t ne = min(g->n_exc, (uint32_t)kGammaExc);
     uint32_t o = 255u << 24;
 #pragma unroll 1
     for (int k = 0; k < 3; ++k) {
@@ -1172,31 +1201,28 @@ __global__ __launch_bounds__(64) void preview_kernel(const FinalizeParams p, con
         if (p.tone_map == 1) tm = js_max<double>(0.0, (x * (2.51 * x + 0.03)) / (x * (2.43 * x + 0.59) + 0.14));
         else if (p.tone_map == 2) tm = x;
         else tm = x / (1.0 + x);
-        // the number of thresholds <= tm (T ascending; a NaN tm passes none)
-        uint32_t lo = 0, n = 255;
-        while (n > 0) {
-            const uint32_t h = n >> 1;
-            if (T[lo + h] <= tm) { lo += h + 1; n -= h + 1; }
-            else n = h;
-        }
-        o |= lo << (8 * k);
+        uint32_t b = gamma_count(g->t, tm);
+        for (uint32_t e = 0; e < ne; ++e)        // the values next to a threshold where pow is not monotone
+            if (g->exc_tm[e] == tm) b = g->exc_byte[e];
+        o |= b << (8 * k);
     }
     *reinterpret_cast<uint32_t*>(rgba8 + 4 * q) = o;
 }
 
-// thresholds of gamma_byte for this gamma (255 doubles); false when 1/gamma is not a finite positive
-// number (the byte is then not a non-decreasing function of tm, and previews take finalize_kernel)
+// thresholds of gamma_byte for this gamma; false when 1/gamma is not a finite positive number (the byte is
+// then not a non-decreasing function of tm, and previews take finalize_kernel)
 bool preview_thresholds_ok(double gamma) {
     const double ig = 1.0 / gamma;
     return ig > 0.0 && ig < INFINITY;
 }
-hipError_t launch_gamma_thresholds(double gamma, double* T, hipStream_t stream) {
+hipError_t launch_gamma_thresholds(double gamma, GammaTable* T, hipStream_t stream) {
     hipLaunchKernelGGL(gamma_thresholds_kernel, dim3(1), dim3(256), 0, stream, 1.0 / gamma, T);
+    hipLaunchKernelGGL(gamma_exceptions_kernel, dim3(255), dim3(256), 0, stream, 1.0 / gamma, T);
     return hipGetLastError();
 }
 
 hipError_t launch_finalize(const FinalizeParams& p, const double* sum, double* mean, float* post, uint8_t* rgba8,
-                           hipStream_t stream, const double* thresholds) {
+                           hipStream_t stream, const GammaTable* thresholds) {
     if (p.n <= 0) return hipSuccess;
     if (thresholds && !mean && !post && rgba8)
         hipLaunchKernelGGL(preview_kernel, dim3((p.n + 63) / 64), dim3(64), 0, stream, p, sum, thresholds, rgba8);

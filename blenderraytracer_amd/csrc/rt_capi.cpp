@@ -314,8 +314,11 @@ struct rt_scene {
     std::vector<uint8_t*> preview_dev;    // the same buffers' device addresses
     size_t preview_host_n = 0;
     std::vector<hipEvent_t> batch_done;   // home stream: batch k's reduce, merges and preview done (slot k % ring)
-    DevBuf<double> gamma_t;         // preview frames: the 255 RGBA8 thresholds of gamma gamma_t_of (launch_gamma_thresholds)
+    // preview frames / RGBA8-only epilogues: the gamma table of gamma gamma_t_of (launch_gamma_thresholds)
+    // and whether it can be used (no exception overflow)
+    DevBuf<unsigned char> gamma_t;
     double gamma_t_of = NAN;
+    bool gamma_t_ok = false;
     std::atomic<int> cancel{0};
     uint32_t* ctl = nullptr;        // the render's control words (kCtl*), host address
     uint32_t* ctl_dev = nullptr;    // ... their device address (portable mapping: valid on every device)
@@ -351,21 +354,36 @@ int check_settings(const rt_settings* s, int* cw, int* ch) {
     return RT_OK;
 }
 
+// The gamma table of `gamma` on the scene's device (built once per gamma on `st`, which is waited for, and
+// its exception count read back), or nullptr when previews must take finalize_kernel
+const GammaTable* gamma_table(rt_scene* sc, double gamma, hipStream_t st) {
+    if (!preview_thresholds_ok(gamma)) return nullptr;
+    if (!(sc->gamma_t_of == gamma)) {
+        uint32_t words[2] = {0, 1};
+        hipError_t e = sc->gamma_t.ensure(sizeof(GammaTable));
+        GammaTable* g = reinterpret_cast<GammaTable*>(sc->gamma_t.p);
+        if (e == hipSuccess) e = launch_gamma_thresholds(gamma, g, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(words, &g->n_exc, sizeof words, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            sc->gamma_t_of = NAN;
+            return nullptr;
+        }
+        sc->gamma_t_of = gamma;
+        sc->gamma_t_ok = words[1] == 0;
+    }
+    return sc->gamma_t_ok ? reinterpret_cast<const GammaTable*>(sc->gamma_t.p) : nullptr;
+}
+
 // mean, toneMap, gammaCorrect (+ PostProcessor.denoise), RGBA8 on `st` (ray-tracer.js:208-276).
-// thresholds: an RGBA8-only epilogue through the gamma thresholds (preview_kernel: the same bytes, 29
-// VGPRs instead of finalize_kernel's 80); the table is built, once per gamma, on `st` and waited for
+// thresholds: an RGBA8-only epilogue through the gamma table (preview_kernel: the same bytes, 29 VGPRs
+// instead of finalize_kernel's 80)
 hipError_t epilogue(rt_scene* sc, const rt_settings* s, int cw, int ch, const double* sum, double* mean, float* post,
                     uint8_t* rgba, hipStream_t st, bool thresholds = false) {
     FinalizeParams fp{cw * ch, s->samples, s->tone_map, s->exposure, s->gamma};
-    if (thresholds && !s->denoise && !mean && !post && rgba && preview_thresholds_ok(s->gamma)) {
-        hipError_t e = sc->gamma_t.ensure(255);
-        if (e == hipSuccess && !(sc->gamma_t_of == s->gamma)) {
-            e = launch_gamma_thresholds(s->gamma, sc->gamma_t.p, st);
-            if (e == hipSuccess) e = hipStreamSynchronize(st);
-            if (e == hipSuccess) sc->gamma_t_of = s->gamma;
-        }
-        return e == hipSuccess ? launch_finalize(fp, sum, nullptr, nullptr, rgba, st, sc->gamma_t.p) : e;
-    }
+    if (thresholds && !s->denoise && !mean && !post && rgba)
+        if (const GammaTable* g = gamma_table(sc, s->gamma, st)) return launch_finalize(fp, sum, nullptr, nullptr, rgba, st, g);
     if (!s->denoise) return launch_finalize(fp, sum, mean, post, rgba, st);
     hipError_t e = sc->post_raw.ensure(4 * (size_t)cw * ch);
     if (e == hipSuccess) e = launch_finalize(fp, sum, mean, sc->post_raw.p, nullptr, st);
@@ -1101,15 +1119,10 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         }
     }
     // the running frames' RGBA8 thresholds for this gamma (exact bytes without a binary64 pow: preview_kernel)
-    const double* thresholds = nullptr;
-    if (want_preview && preview_thresholds_ok(s->gamma)) {
+    const GammaTable* thresholds = nullptr;
+    if (want_preview) {
         HIP_TRY(hipSetDevice(h.device));
-        HIP_TRY(sc->gamma_t.ensure(255));
-        if (!(sc->gamma_t_of == s->gamma)) {
-            HIP_TRY(launch_gamma_thresholds(s->gamma, sc->gamma_t.p, h.stream));
-            sc->gamma_t_of = s->gamma;
-        }
-        thresholds = sc->gamma_t.p;
+        thresholds = gamma_table(sc, s->gamma, h.stream);
     }
     sc->ckpt_pixels = n;
     sc->ckpt_done = s0;

@@ -578,8 +578,9 @@ void make_records(const HostScene& hs, const rt_scene_desc& d, HostRecords<R>& o
     for (size_t i = 0; i < out.sphere_filter.size(); ++i) {
         const double* s = &hs.spheres[4 * i];
         const double k = 2.0 * (s[0] * s[0] + s[1] * s[1] + s[2] * s[2]) + s[3];
-        // r2p = r^2 + 2^-17 k, rounded up (sphere_filter_bound in pt_core.h)
-        out.sphere_filter[i] = SphereFilter{(float)s[0], (float)s[1], (float)s[2], (float)((s[3] + 0x1p-17 * k) * (1.0 + 0x1p-20))};
+        // r2p = r^2 + 2^RT_FILTER_MARGIN k, rounded up (sphere_filter_bound in pt_core.h)
+        out.sphere_filter[i] = SphereFilter{(float)s[0], (float)s[1], (float)s[2],
+                                            (float)((s[3] + filter_margin() * k) * (1.0 + 0x1p-20))};
     }
     out.planes.resize(hs.plane_mat.size());
     for (size_t i = 0; i < out.planes.size(); ++i) {

@@ -115,7 +115,7 @@ extern "C" int ptc_sphere_filter_check(long long n, unsigned seed, double* max_r
         const double cc = (ocx * ocx + ocy * ocy + ocz * ocz) - r * r;
         const double disc64 = hb * hb - a * cc;
         const double k = 2.0 * (c[0] * c[0] + c[1] * c[1] + c[2] * c[2]) + r * r;
-        SphereFilter f{(float)c[0], (float)c[1], (float)c[2], (float)((r * r + 0x1p-17 * k) * (1.0 + 0x1p-20))};
+        SphereFilter f{(float)c[0], (float)c[1], (float)c[2], (float)((r * r + filter_margin() * k) * (1.0 + 0x1p-20))};
         const FilterRay fr = make_filter_ray(V3<double>{o[0], o[1], o[2]}, V3<double>{d[0], d[1], d[2]});
         const bool pass = sphere_filter_pass(f, fr);
         if (disc64 >= 0 && !pass) ++violations;

@@ -89,7 +89,8 @@ def bvh_rays(packed, n, seed, host_n=None):
 
 
 EVENTS = ["f64_sphere_tests", "disc_nonneg", "second_root", "accept", "lambertian", "metal", "dielectric", "emissive",
-          "miss", "samples", "sphere_draw_rounds", "disk_draw_rounds", "filter_tests", "dielectric_schlick"]
+          "miss", "samples", "sphere_draw_rounds", "disk_draw_rounds", "filter_tests", "dielectric_schlick",
+          "tri_filter_tests", "tri_tests"]
 
 
 def event_counts(packed, settings_list, walk):

@@ -177,7 +177,10 @@ def test_js_gpu_render_matches_reference(gpu):
         cl = summary["_cancelLatency"]
         print(f"Node cancel-to-return {cl['latencyMs']:.2f} ms, frame {cl['frameMs']:.1f} ms, "
               f"checkpoint {cl['samplesDone']} of 512 samples")
-        assert cl["latencyMs"] < cl["frameMs"] / 4 and cl["samplesDone"] in (128, 256, 384), cl
+        # round 5: the checkpoint's sums stay on the device until read (checkpointState is lazy), so
+        # the cancel returns after the kernels stop and the frame of the checkpoint is copied: 8.1 ms
+        # measured (round 4, with the 50-MB copy: 24.6 ms)
+        assert cl["latencyMs"] < cl["frameMs"] / 8 and cl["samplesDone"] in (128, 256, 384), cl
 
 
 def test_pow5_vs_v8_math_pow(tmp_path):
