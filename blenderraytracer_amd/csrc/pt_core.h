@@ -256,6 +256,14 @@ struct Closest { R t; int kind, idx, mat, obj; };   // obj: World.objects index 
 #define RT_PRAGMA(x) _Pragma(#x)
 #define RT_UNROLL(n) RT_PRAGMA(unroll n)
 
+#ifndef RT_LEAVE_ALL
+#define RT_LEAVE_ALL 0
+#endif
+template <class R> RT_HD bool sphere_leaves(R hb, R c, R a, R tmin) {
+    return hb >= (R)0 &&
+           (c >= (R)0 || (-c < hb * (tmin * (R)0.25) && hb * (R)(sizeof(R) == 8 ? 0x1p-45 : 0x1p-18) < a * (tmin * (R)0.25)));
+}
+
 // Sphere.hit (geometry.js:15-45) folded into World.hit's strict-< acceptance, in R arithmetic.
 template <class R>
 RT_HD void sphere_test_f64(const SceneView<R>& sc, V3<R> o, V3<R> d, R a, R tmin, int i, Closest<R>& b) {
@@ -263,6 +271,7 @@ RT_HD void sphere_test_f64(const SceneView<R>& sc, V3<R> o, V3<R> d, R a, R tmin
     R ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
     R hb = ocx * d.x + ocy * d.y + ocz * d.z;
     R c = (ocx * ocx + ocy * ocy + ocz * ocz) - s.r2;
+    if (RT_LEAVE_ALL && sphere_leaves<R>(hb, c, a, tmin)) return;   // both roots below tmin (pt_core.h `leave`)
     R disc = hb * hb - a * c;
     if (disc < (R)0) return;
     R sq = sqrt(disc);
@@ -435,6 +444,16 @@ RT_HD bool better(R t, int obj, int id, const Closest<R>& b) {
 // = hb, so sqrt(disc) <= hb, both roots are <= 0 < tmin, and the reference's test rejects as well (NaN
 // operands fail the comparisons and take the full test).  Used for the dominant spheres, which every
 // ray leaving them (the RTOW ground: most secondary rays) would otherwise test in full: +0.9 %.
+// leave (round 5): the same for an origin just INSIDE the sphere (c < 0, the hit point of the previous
+// segment rounded inwards) moving away from the centre (hb > 0): the near root is negative and the far
+// one t2 = RN(RN(-hb + sq) / a) with sq = RN(sqrt(RN(RN(hb^2) + RN(a |c|)))) <= (1+u)^2 (hb + a|c|/(2hb)),
+// so t2 <= (1+u)^4 (2.01u hb / a + |c| / (2 hb)).  With |c| < hb tmin / 4 and hb 2^-45 < a tmin / 4
+// (binary32: 2^-18) that is below tmin / 7: both roots fail `root < tMin`, as in the reference.  This is
+// every ray leaving a sphere it was scattered from, whose second root the full test computes (RTOW: 0.46
+// second roots per segment, host count).  RT_LEAVE_ALL: both rules for every sphere — measured slower
+// (RTOW 256 spp f64 10261 vs 10347, f32 -1.2 %, Cornell and mesh50k +-0.5 %: the lanes that skip still wait
+// for the survivor loop's other lanes), so 0: the dominant spheres (their `away` flag) only
+
 // RT_ROOT_RCP: the roots' divisions by a = d.d as Markstein corrections from ya = RN(1/a), computed
 // once per closest-hit query (the grid walk; ya = 0: the plain divisions), guarded so that every
 // intermediate is normal: 2^-500 <= |-hb -+ sqrt(disc)| <= 2^500 (the caller: 2^-400 <= a <= 2^400;
@@ -462,7 +481,7 @@ RT_HD bool sphere_candidate(const SphereRec<R>& s, V3<R> o, V3<R> d, R a, R tmin
     R ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
     R hb = ocx * d.x + ocy * d.y + ocz * d.z;
     R c = (ocx * ocx + ocy * ocy + ocz * ocz) - s.r2;
-    if (away && c >= (R)0 && hb >= (R)0) return false;
+    if ((away || RT_LEAVE_ALL) && sphere_leaves<R>(hb, c, a, tmin)) return false;
     R disc = hb * hb - a * c;
     if (disc < (R)0) return false;
     RT_HCOUNT(HC_DISC_OK, 1);
@@ -826,6 +845,7 @@ RT_HD void sphere_records(const SphereLeaf<R>* recs, int first, int end, V3<R> o
         R t;
         if (!sphere_candidate(L.s, o, d, a, tmin, t, away, ya)) continue;
         if (better(t, L.obj, L.id, b)) {
+            RT_HCOUNT(HC_ACCEPT, 1);
             b = Closest<R>{t, HIT_SPHERE, L.id, L.mat, L.obj};
             tl = bvh_tlimit(b.t);
         }
@@ -975,6 +995,7 @@ RT_HD void sphere_records_lds(const rt_u4* lrec, const SphereLeaf<R>* recs, int 
                 R t;
                 if (!sphere_candidate(s, o, d, a, tmin, t, false, ya)) continue;
                 if (better(t, obj, id, b)) {
+                    RT_HCOUNT(HC_ACCEPT, 1);
                     b = Closest<R>{t, HIT_SPHERE, id, mat, obj};
                     tl = bvh_tlimit(b.t);
                 }
@@ -1000,6 +1021,7 @@ RT_HD void sphere_records_lds(const rt_u4* lrec, const SphereLeaf<R>* recs, int 
         R t;
         if (!sphere_candidate(s, o, d, a, tmin, t, false, ya)) continue;
         if (better(t, obj, id, b)) {
+            RT_HCOUNT(HC_ACCEPT, 1);
             b = Closest<R>{t, HIT_SPHERE, id, mat, obj};
             tl = bvh_tlimit(b.t);
         }

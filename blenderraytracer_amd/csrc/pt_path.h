@@ -47,6 +47,9 @@ RT_COLD_HD AaUv<R> stochastic_uv(uint32_t key, int i, int j, int width, int heig
     return AaUv<R>{((R)i + (R)0.5 + ox * (R)0.5) / (R)width, ((R)j + (R)0.5 + oy * (R)0.5) / (R)height};
 }
 
+#ifndef RT_OPAQUE_WH
+#define RT_OPAQUE_WH 0
+#endif
 template <class R>
 RT_HD void start_sample(const SceneView<R>& sc, const ImageParams& im, int i, int j, uint32_t pkey, int s, Rng<R>& g,
                         V3<R>& o, V3<R>& d) {
@@ -54,17 +57,26 @@ RT_HD void start_sample(const SceneView<R>& sc, const ImageParams& im, int i, in
     g.key = sample_key(pkey, (uint32_t)s);
     g.k = 0;
     R u, v;                                                                   // ray-tracer.js:125-149
+#if RT_OPAQUE_WH && defined(__HIP_DEVICE_COMPILE__)
+    // (R)width / (R)height converted here from the kernel-argument SGPRs at every sample start instead of
+    // hoisted out of the pool loop by the compiler (they then live in scratch): A/B
+    int iw = im.width, ih = im.height;
+    asm volatile("" : "+s"(iw), "+s"(ih));
+    const R width = (R)iw, height = (R)ih;
+#else
+    const R width = (R)im.width, height = (R)im.height;
+#endif
     if (im.aa_mode == 1) {
         const AaUv<R> uv = stochastic_uv<R>(g.key, i, j, im.width, im.height);
         u = uv.u;
         v = uv.v;
         g.k = 2;
     } else if (im.aa_mode == 0) {
-        u = ((R)i + g.next()) / (R)im.width;
-        v = ((R)j + g.next()) / (R)im.height;
+        u = ((R)i + g.next()) / width;
+        v = ((R)j + g.next()) / height;
     } else {
-        u = ((R)i + (R)0.5) / (R)im.width;
-        v = ((R)j + (R)0.5) / (R)im.height;
+        u = ((R)i + (R)0.5) / width;
+        v = ((R)j + (R)0.5) / height;
     }
     const V3<R> cu = mk(sc.cam_u[0], sc.cam_u[1], sc.cam_u[2]);               // camera.js:38-51
     const V3<R> cv = mk(sc.cam_vv[0], sc.cam_vv[1], sc.cam_vv[2]);
@@ -103,6 +115,44 @@ RT_HD R pow5_rn(R x) {
     return r + re;
 }
 
+// Dielectric.scatter (materials.js:51-83) by value (RT_COLD_DIEL: out of line, so its registers leave the
+// trace kernel's allocation — A/B): the new direction and the RNG's draw count
+template <class R> struct DielOut { V3<R> nd; uint32_t k; };
+#ifndef RT_COLD_DIEL
+#define RT_COLD_DIEL 0
+#endif
+#if RT_COLD_DIEL && defined(__HIP_DEVICE_COMPILE__)
+#define RT_DIEL_HD __host__ __device__ __attribute__((noinline))
+#else
+#define RT_DIEL_HD RT_HD
+#endif
+template <class R>
+RT_DIEL_HD DielOut<R> dielectric_scatter(R inv_ior, R ior, R r0f, R r0b, bool front, V3<R> n, V3<R> unit, uint32_t key,
+                                         uint32_t k) {
+    Rng<R> g{key, k};
+    V3<R> nd;
+    // 1 / ior and both faces' r0 come precomputed (scene_pack.h, the same roundings): two divisions fewer
+    R ratio = front ? inv_ior : ior;
+    R cos_t = js_min<R>(dot(unit * (R)-1, n), (R)1);
+    R sin_t = sqrt((R)1 - cos_t * cos_t);
+    bool reflect_it = ratio * sin_t > (R)1;
+    if (!reflect_it) {                                                        // random drawn only if it can refract
+        RT_HCOUNT(HC_DIELECTRIC_SCHLICK, 1);
+        const R r0 = front ? r0f : r0b;
+        R refl = r0 + ((R)1 - r0) * pow5_rn((R)1 - cos_t);
+        reflect_it = refl > g.next();
+    }
+    if (reflect_it) {
+        nd = reflect(unit, n);
+    } else {
+        R ct = js_min<R>(dot(unit * (R)-1, n), (R)1);
+        V3<R> perp = (unit + n * ct) * ratio;
+        V3<R> par = n * (-sqrt(fabs((R)1 - dot(perp, perp))));
+        nd = perp + par;
+    }
+    return DielOut<R>{nd, g.k};
+}
+
 // Scatter at a non-emissive hit (materials.js:20-83).  Returns false when Metal absorbs.
 // The three materials share their common steps so that a wave holding several of them runs each step
 // once (a branch runs for the union of its lanes): Lambertian and Metal draw one randomInUnitSphere
@@ -129,26 +179,10 @@ RT_HD bool scatter(const MatRec<R>& m, const Hit<R>& h, V3<R> unit, V3<R> p, Rng
     att = mk<R>(1, 1, 1);
     return true;
 #endif
-    // Dielectric :51-83 (ior): 1 / ior and both faces' r0 come precomputed in c[] (scene_pack.h, the same
-    // roundings): two divisions fewer per dielectric hit
-    R ratio = h.front ? m.c[0] : m.p;
-    R cos_t = js_min<R>(dot(unit * (R)-1, h.n), (R)1);
-    R sin_t = sqrt((R)1 - cos_t * cos_t);
-    bool reflect_it = ratio * sin_t > (R)1;
-    if (!reflect_it) {                                                        // random drawn only if it can refract
-        RT_HCOUNT(HC_DIELECTRIC_SCHLICK, 1);
-        const R r0 = h.front ? m.c[1] : m.c[2];
-        R refl = r0 + ((R)1 - r0) * pow5_rn((R)1 - cos_t);
-        reflect_it = refl > g.next();
-    }
-    if (reflect_it) {
-        nd = reflect(unit, h.n);
-    } else {
-        R ct = js_min<R>(dot(unit * (R)-1, h.n), (R)1);
-        V3<R> perp = (unit + h.n * ct) * ratio;
-        V3<R> par = h.n * (-sqrt(fabs((R)1 - dot(perp, perp))));
-        nd = perp + par;
-    }
+    // Dielectric :51-83 (ior)
+    const DielOut<R> r = dielectric_scatter<R>(m.c[0], m.p, m.c[1], m.c[2], h.front, h.n, unit, g.key, g.k);
+    nd = r.nd;
+    g.k = r.k;
     att = mk<R>(1, 1, 1);
     return true;
 }

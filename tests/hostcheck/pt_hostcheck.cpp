@@ -137,10 +137,25 @@ extern "C" int ptc_sphere_filter_check(long long n, unsigned seed, double* max_r
     return (int)violations;
 }
 
-// Away-rejection (sphere_candidate's `away`): rays leaving a sphere's surface — the origin is the hit
-// point o + t d of a previous ray computed in binary64, the new direction random (outward, inward,
-// grazing) — and random rays elsewhere.  Returns the number of cases where the rejection changes the
-// decision or t of the full test; *taken counts the cases it rejected early.
+// The reference's Sphere.hit decision and root (geometry.js:15-45) in binary64, without any early rule
+static bool sphere_full(const SphereRec<double>& s, V3<double> o, V3<double> d, double a, double tmin, double& t) {
+    const double ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
+    const double hb = ocx * d.x + ocy * d.y + ocz * d.z;
+    const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - s.r2;
+    const double disc = hb * hb - a * c;
+    if (disc < 0) return false;
+    const double sq = std::sqrt(disc);
+    t = (-hb - sq) / a;
+    if (!(t < tmin)) return true;
+    t = (-hb + sq) / a;
+    return !(t < tmin);
+}
+
+// Away and leave rejections (sphere_candidate's early rules): rays leaving a sphere's surface — the
+// origin is the hit point o + t d of a previous ray computed in binary64 (just inside or just outside),
+// the new direction random (outward, inward, grazing) — and random rays elsewhere, at 8 decades of scale.
+// Returns the number of cases where sphere_candidate's decision or t differs from the full test;
+// *taken counts the cases an early rule rejected (full test: a miss that computed a root).
 extern "C" long long ptc_away_check(long long n, unsigned seed, long long* taken) {
     std::mt19937_64 gen(seed);
     std::uniform_real_distribution<double> U(-1.0, 1.0);
@@ -166,10 +181,11 @@ extern "C" long long ptc_away_check(long long n, unsigned seed, long long* taken
         const double a = dot(d, d);
         double ta = 0, tb = 0;
         const bool ha = sphere_candidate(s, o, d, a, 0.001, ta, true);
-        const bool hb = sphere_candidate(s, o, d, a, 0.001, tb, false);
+        const bool hb = sphere_full(s, o, d, a, 0.001, tb);
         if (ha != hb || (ha && ta != tb)) ++bad;
         const V3<double> oc = o - mk(s.cx, s.cy, s.cz);
-        early += (oc.x * oc.x + oc.y * oc.y + oc.z * oc.z) - s.r2 >= 0 && oc.x * d.x + oc.y * d.y + oc.z * d.z >= 0;
+        const double cc = (oc.x * oc.x + oc.y * oc.y + oc.z * oc.z) - s.r2, hh = oc.x * d.x + oc.y * d.y + oc.z * d.z;
+        early += hh >= 0 && (cc >= 0 || (-cc < hh * 0.00025 && hh * 0x1p-45 < a * 0.00025));
     }
     *taken = early;
     return bad;

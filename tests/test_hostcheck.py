@@ -108,10 +108,11 @@ def test_dominant_spheres_rtow():
 
 
 def test_away_rejection_is_exact():
-    """sphere_candidate's early rejection (origin outside or on the sphere, moving away) never changes
-    the full binary64 test's decision or t: 2 M rays, half of them leaving a sphere from a binary64
-    hit point (a quarter nearly tangent), radii from 1e-3 to 1e7 including the RTOW ground's R = 1000
-    and negative radii."""
+    """sphere_candidate's early rejections (origin outside or on the sphere moving away; origin just
+    inside it moving away, the far root then below tMin — pt_core.h `leave`) never change the decision or
+    t of the reference's full binary64 test (geometry.js:15-45, restated in the host check): 2 M rays,
+    half of them leaving a sphere from a binary64 hit point (a quarter nearly tangent), radii from 1e-3 to
+    1e7 including the RTOW ground's R = 1000 and negative radii."""
     import ctypes as C
     taken = C.c_longlong()
     assert hb.lib().ptc_away_check(2_000_000, 11, C.byref(taken)) == 0
