@@ -59,15 +59,9 @@ RT_HD unsigned pool_position(unsigned b, unsigned n) {
         return g * 8 * K + (r & 7) * K + (r >> 3);
     }
 }
-// item (chunk * tiles + tile) at position p of the visiting order.  im.tile_order (longest-first): the
-// tiles of every chunk in the order of their estimated cost, most expensive first, so that a launch
-// ends on its cheapest items and its waves drain together (rt_capi.cpp tile_order; a permutation too)
+// item (chunk * tiles + tile) at position p of the visiting order.  (A longest-first order of each
+// chunk's tiles, from a host estimate of the frame's cost, measured slower in round 5: DESIGN.md §4.)
 RT_HD unsigned item_at(const ImageParams& im, unsigned p, int tiles) {
-    if (im.tile_order) {
-        const unsigned ci = p / (unsigned)tiles;
-        if ((int)ci >= im.order_chunk0) return ci * (unsigned)tiles + (unsigned)im.tile_order[p - ci * (unsigned)tiles];
-        if constexpr (RT_TILE_BLOCK <= 1) return p;
-    }
     if constexpr (RT_TILE_BLOCK <= 1) return p;
     const unsigned ci = p / (unsigned)tiles;
     return ci * (unsigned)tiles + (unsigned)tile_at(im, (int)(p - ci * (unsigned)tiles));
@@ -79,7 +73,7 @@ RT_HD ChunkRange chunk_range(const ImageParams& im, int gci, int chunk) {
     ChunkRange r;
     r.b = im.batch_chunks ? gci / im.batch_chunks : 0;
     r.ci = gci - r.b * im.batch_chunks;
-    const int bs = im.s_begin + r.b * (im.batch_stride > 0 ? im.batch_stride : im.batch_samples);
+    const int bs = im.s_begin + r.b * im.batch_samples * (im.batch_ways > 1 ? im.batch_ways : 1);
     r.sb = bs + r.ci * chunk;
     r.se = min(im.batch_chunks ? min(im.s_end, bs + im.batch_samples) : im.s_end, r.sb + chunk);
     return r;

@@ -259,7 +259,11 @@ struct Closest { R t; int kind, idx, mat, obj; };   // obj: World.objects index 
 #ifndef RT_LEAVE_ALL
 #define RT_LEAVE_ALL 0
 #endif
+#ifndef RT_LEAVE_INSIDE
+#define RT_LEAVE_INSIDE 1         // 0 (A/B): round 4's away rule only (c >= 0)
+#endif
 template <class R> RT_HD bool sphere_leaves(R hb, R c, R a, R tmin) {
+    if (!RT_LEAVE_INSIDE) return hb >= (R)0 && c >= (R)0;
     return hb >= (R)0 &&
            (c >= (R)0 || (-c < hb * (tmin * (R)0.25) && hb * (R)(sizeof(R) == 8 ? 0x1p-45 : 0x1p-18) < a * (tmin * (R)0.25)));
 }

@@ -22,9 +22,11 @@ struct Counters {
     unsigned long long* totals;   // optional [segments, BVH nodes, sphere tests, triangle tests]
     double* part = nullptr;    // sample-pool chunk partials (scratch, pool_partial_bytes)
     size_t part_bytes = 0;
-    // progressive renders (render_impl): the render's cancel word in mapped host memory, read by the pool
-    // kernels before every (tile, chunk) item; a wave that finds it set leaves its items untraced and
-    // sets *aborted (this batch's word, mapped host memory too), so that the batch is never reduced.
+    // progressive renders (render_impl): the render's cancel word in mapped host memory.  The one-wave
+    // pool kernel reads it as each (tile, chunk) item starts; a workgroup that finds it set leaves its
+    // item untraced and sets *aborted (this batch's word, mapped host memory too), so that the batch is
+    // never reduced.  The LDS pool kernels read no cancel word: their launches are registered under it,
+    // and cancel_pool_launches(cancel) moves their queues past the last item (and sets *aborted).
     // kCancelCopies copies of the word, one per 128-B line (cancel[k * kCancelStride]), the host writes
     // all of them: the waves' reads spread over many lines instead of queueing on one
     const uint32_t* cancel = nullptr;
@@ -33,8 +35,7 @@ struct Counters {
     // launch) and the flag the item completing the batch raises (mapped host memory: the host enqueues
     // the batch's reduce once it is set, and its gate commits the batch only if it is set)
     uint32_t* batch_count = nullptr;
-    uint32_t* batch_flag = nullptr;
-    int flag_stride = 1;       // the flag of the launch's batch b at batch_flag[b * flag_stride]
+    uint32_t* batch_flag = nullptr;      // batch b's flag: batch_flag[b * ImageParams::batch_ways]
 };
 constexpr int kCancelCopies = 128, kCancelStride = 32;
 
@@ -73,12 +74,22 @@ hipError_t launch_trace_partials(const SceneView<R>& sc, const ImageParams& im, 
 hipError_t launch_reduce(const ImageParams& im, double* sum, const double* part, bool tri_bvh, hipStream_t stream,
                          const ReduceGate* gate = nullptr);
 // All batches of a progressive render in ONE pool launch (items batch-major in the pool's queue): batch
-// b = samples [im.s_begin + b * stride, + batch) (stride = im.batch_stride, or batch) into part + b *
+// b = samples [im.s_begin + b * stride, + batch) (stride = batch x im.batch_ways) into part + b *
 // fused_batch_doubles(...), each batch's items signalled through c.batch_count / c.batch_flag.  The same items, chunks and partials as one
 // launch_trace_partials per batch, so launch_reduce of each batch's partials adds the same bits.
 template <class R>
 hipError_t launch_trace_batches(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh, int batch,
                                 double* part, size_t part_bytes, hipStream_t stream);
+// The LDS pool launches of a render (Counters::cancel != nullptr) are registered under its cancel word
+// until forget_pool_launches(cancel).  cancel_pool_launches(cancel): for each registered launch not yet
+// cancelled, set its `aborted` word, then move its queue past the last item (a one-thread kernel on a
+// high-priority stream of the launch's device, beside the trace waves), so that every wave's next take
+// ends its loop; the items already taken finish.  A queue moved after its launch ended is zeroed again
+// on the launch's stream.  Thread-safe (rt_cancel calls it from any thread); the caller's current
+// device is kept.  A launch cancelled after all its items were taken still counts as aborted.
+hipError_t cancel_pool_launches(const uint32_t* cancel);
+void forget_pool_launches(const uint32_t* cancel);
+
 // doubles of one batch's partials in a fused launch, and the items that complete it
 size_t fused_batch_doubles(int cw, int ch, int batch, bool tri_bvh, int chunk);
 uint32_t fused_batch_items(int cw, int ch, int batch, bool tri_bvh, int chunk);

@@ -25,13 +25,10 @@ struct ImageParams {
     // s_begin, batch_chunks chunks each, batch-major (chunk index c of the launch = batch c / batch_chunks);
     // 0: one batch
     int batch_samples, batch_chunks;
-    // samples from one batch's start to the next one's (0: batch_samples) — a device's batches of the
-    // whole-batch multi-device split are every N-th batch of the render
-    int batch_stride;
-    // the pool's tile visiting order within each chunk (device array of the crop's tiles, most expensive
-    // first: rt_capi.cpp tile_order), or nullptr for raster order (pool_order.h item_at)
-    const int* tile_order;
-    int order_chunk0;          // the order applies to the launch's chunks >= this (-1: its last chunk only)
+    // the whole-batch multi-device split (rt_capi.cpp): the launch's batches are every batch_ways-th batch
+    // of the render (batch b starts batch_ways * batch_samples samples after batch b - 1, and raises the
+    // flag batch_flag[b * batch_ways]); 0 or 1: consecutive batches
+    int batch_ways;
 };
 
 // Stochastic AA offsets (ray-tracer.js:136-141): sqrt, cos and sin in binary64 are long code that

@@ -15,6 +15,8 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "pt_launch.h"
 #include "pool_order.h"
@@ -113,12 +115,10 @@ __device__ __forceinline__ void add_totals(const Counters& c, const PixelResult&
 #ifndef RT_CANCEL_POLL
 #define RT_CANCEL_POLL 1          // A/B: 0 = the kernels never read the cancel word (the gates still run)
 #endif
-// The LDS pool kernel's wave 0 reads the cancel word before every RT_CANCEL_EVERY-th item of its own (a
-// read of mapped host memory stalls the wave for its PCIe round trip; config 3 in 16 fused batches:
-// every item +3.5 %), the workgroup's other waves read its LDS flag before every item
-#ifndef RT_CANCEL_EVERY
-#define RT_CANCEL_EVERY 4
-#endif
+// The one-wave pool kernel reads it as its workgroup (= one item) starts; the LDS pool kernel reads no
+// cancel word at all (cancel_pool_launches moves its queue instead: a poll inside its item loop, even
+// one read per 16 queue positions, cost config 3's 16 fused batches 3-5 % through the kernel's
+// register allocation).
 // copy: the wave's copy of the word (Counters::cancel); one line read by every wave measured 50 us per
 // read (RTOW 16 progressive batches: +4.5 % kernel time), the reads of one line being serialized
 __device__ __forceinline__ bool cancel_requested(const Counters& c, unsigned copy) {
@@ -158,7 +158,7 @@ __device__ __forceinline__ void store_through(double* p, double v) {
 #ifndef RT_COMMIT_FENCE
 #define RT_COMMIT_FENCE 1
 #endif
-__device__ __forceinline__ void item_done(const Counters& c, int b, uint32_t batch_items, int lane) {
+__device__ __forceinline__ void item_done(const Counters& c, int b, uint32_t batch_items, int ways, int lane) {
 #if RT_COMMIT_FENCE
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __builtin_amdgcn_wave_barrier();
@@ -167,7 +167,7 @@ __device__ __forceinline__ void item_done(const Counters& c, int b, uint32_t bat
                                                   __HIP_MEMORY_SCOPE_AGENT);
         if (k + 1 == batch_items) {
             if (RT_COMMIT_FENCE != 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            __hip_atomic_store(c.batch_flag + b * c.flag_stride, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(c.batch_flag + b * (ways > 1 ? ways : 1), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 #else
@@ -175,7 +175,7 @@ __device__ __forceinline__ void item_done(const Counters& c, int b, uint32_t bat
     if (lane == 0) {
         const uint32_t k = __hip_atomic_fetch_add(c.batch_count + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k + 1 == batch_items)
-            __hip_atomic_store(c.batch_flag + b * c.flag_stride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(c.batch_flag + b * (ways > 1 ? ways : 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 #endif
 }
@@ -403,7 +403,7 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
             args.c.sum[3 * qq + 2] += acc[128 + lane];
         }
     }
-    if (args.c.batch_count) item_done(args.c, cr.b, (uint32_t)(im.batch_chunks * tiles), lane);
+    if (args.c.batch_count) item_done(args.c, cr.b, (uint32_t)(im.batch_chunks * tiles), im.batch_ways, lane);
     add_totals<ACC>(args.c, res, lane);
 }
 
@@ -507,7 +507,7 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
             args.c.sum[3 * qq + 2] += acc[128 + lane];
         }
     }
-    if (args.c.batch_count) item_done(args.c, cr.b, (uint32_t)(im.batch_chunks * tiles), lane);
+    if (args.c.batch_count) item_done(args.c, cr.b, (uint32_t)(im.batch_chunks * tiles), im.batch_ways, lane);
     acc[lane] = 0;                            // the wave's next item starts from zero partials
     acc[64 + lane] = 0;
     acc[128 + lane] = 0;
@@ -565,7 +565,7 @@ __device__ __forceinline__ void copy_nodes_lds(const SceneView<R>& sc, rt_u4* bo
 // ACC_GRID_LDS: the same workgroups and queue with the uniform grid's cell offsets and records
 // (binary64: the 16-B binary32 filters; binary32: the whole 32-B records) in LDS instead of nodes: the
 // filter rejections, most of a grid walk's record tests, no longer touch the vector memory path.
-template <class R, bool COUNT, int ACC, bool CANCEL>
+template <class R, bool COUNT, int ACC>
 __global__ __launch_bounds__((64 * lds_waves<R, ACC>()), (waves_per_simd<R, ACC>()))
 void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, const int tiles, const int chunk,
                            const int items, const int qi) {
@@ -575,9 +575,7 @@ void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, c
     // for the grid [records][cell offsets]
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_dyn[];
     __shared__ double acc_all[W * 3 * 64];
-    __shared__ uint32_t stop_flag;            // CANCEL: wave 0 polls the cancel word, the others read this
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (CANCEL && threadIdx.x == 0) stop_flag = 0;
     BvhStack stk{nullptr, 0};
     if constexpr (ACC == ACC_GRID_LDS) {
         rt_u4* grec = reinterpret_cast<rt_u4*>(lds_dyn);
@@ -608,24 +606,13 @@ void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, c
     __syncthreads();
     uint32_t* queue = g_pool_queue + 2 * qi;
     PixelResult res{0, 0, {0, 0, 0}, {0, 0, 0}};
-    unsigned taken = 0;                       // CANCEL: items this wave has taken
+    // no cancel word is read here: a cancel moves this launch's queue past its last item from outside
+    // (cancel_pool_launches), and every wave's next take ends its loop
     for (;;) {
         uint32_t it = 0;
-        int stop = 0;
-        if (lane == 0) {
-            if constexpr (CANCEL) {
-                if (wave == 0 && taken++ % RT_CANCEL_EVERY == 0 && cancel_requested(args.c, blockIdx.x))
-                    __hip_atomic_store(&stop_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                stop = (int)__hip_atomic_load(&stop_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            it = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (lane == 0) it = __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         it = (uint32_t)__builtin_amdgcn_readfirstlane((int)it);
         if (it >= (uint32_t)items) break;
-        if (CANCEL && __builtin_amdgcn_readfirstlane(stop)) {   // a cancel: this item (and the rest) stay untraced
-            if (lane == 0) mark_aborted(args.c);
-            break;
-        }
         pool_item<R, COUNT, ACC>(args, part, tiles, chunk, it, acc, stk, res, lane, lmats);
     }
     add_totals<ACC>(args.c, res, lane);
@@ -777,6 +764,107 @@ static size_t lds_nodes_bytes(const SceneView<R>& sc) {
 // together (streams, scenes, precisions) never share a queue
 static std::atomic<unsigned> g_next_queue{0};
 
+// ---- cancelling LDS pool launches in flight (pt_launch.h: cancel_pool_launches) ----
+// The queue of launch qi moved to `items`: takes from then on return >= items.  aborted is stored first
+// (system scope, before the move's release), so the batch's gate, which runs after the launch ends and
+// so after a wave has taken a moved position, reads it set.
+__global__ __launch_bounds__(64) void queue_cancel_kernel(const int qi, const uint32_t items, uint32_t* aborted) {
+    if (threadIdx.x != 0) return;
+    if (aborted) __hip_atomic_store(aborted, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope
+    __hip_atomic_fetch_max(g_pool_queue + 2 * qi, items, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// after the launch (and the move) ended: the queue pair back to 0 for the ring's next user
+__global__ __launch_bounds__(64) void queue_clear_kernel(const int qi) {
+    if (threadIdx.x < 2) __hip_atomic_store(g_pool_queue + 2 * qi + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+namespace {
+struct PoolLaunch {
+    const uint32_t* cancel;
+    uint32_t* aborted;
+    int device, qi;
+    uint32_t items;
+    hipStream_t stream;
+    hipEvent_t done;                      // recorded after the launch
+};
+std::mutex g_launch_mu;
+std::vector<PoolLaunch> g_launches;       // launches that may still run (pruned as they are found done)
+hipStream_t g_cancel_stream[64];          // per device, created on first use (under g_launch_mu)
+
+// drop the records for which keep() is false (their events destroyed)
+template <class F>
+void prune_launches(F keep) {
+    size_t w = 0;
+    for (size_t k = 0; k < g_launches.size(); ++k) {
+        if (keep(g_launches[k])) g_launches[w++] = g_launches[k];
+        else if (g_launches[k].done) (void)hipEventDestroy(g_launches[k].done);
+    }
+    g_launches.resize(w);
+}
+bool launch_done(const PoolLaunch& l) { return !l.done || hipEventQuery(l.done) == hipSuccess; }
+}  // namespace
+
+// after the launch was enqueued on `stream` (of the current device).  Records whose launch has ended
+// are dropped here and in cancel_pool_launches: a record is only ever acted on while its launch may
+// still hold its queue slot, never after the ring has handed that slot to another launch
+static hipError_t register_pool_launch(const Counters& c, int qi, uint32_t items, hipStream_t stream) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    hipEvent_t ev = nullptr;
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(ev, stream);
+    if (e != hipSuccess) {
+        if (ev) (void)hipEventDestroy(ev);
+        return e;
+    }
+    std::lock_guard<std::mutex> g(g_launch_mu);
+    prune_launches([](const PoolLaunch& l) { return !launch_done(l); });
+    g_launches.push_back(PoolLaunch{c.cancel, c.aborted, dev, qi, items, stream, ev});
+    return hipSuccess;
+}
+
+hipError_t cancel_pool_launches(const uint32_t* cancel) {
+    if (!cancel) return hipSuccess;
+    std::lock_guard<std::mutex> g(g_launch_mu);
+    int cur = -1;
+    hipError_t err = hipSuccess;
+    prune_launches([&](const PoolLaunch& l) {
+        if (l.cancel != cancel) return !launch_done(l);
+        if (launch_done(l)) return false;
+        if (cur < 0 && hipGetDevice(&cur) != hipSuccess) cur = 0;
+        hipError_t e = hipSetDevice(l.device);
+        hipStream_t& cs = g_cancel_stream[l.device & 63];
+        if (e == hipSuccess && !cs) {
+            int lo = 0, hi = 0;
+            (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+            e = hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, hi);
+        }
+        hipEvent_t ev = nullptr;
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(queue_cancel_kernel, dim3(1), dim3(64), 0, cs, l.qi, l.items, l.aborted);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(ev, cs);
+        if (e == hipSuccess) e = hipStreamWaitEvent(l.stream, ev, 0);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(queue_clear_kernel, dim3(1), dim3(64), 0, l.stream, l.qi);
+            e = hipGetLastError();
+        }
+        if (ev) (void)hipEventDestroy(ev);
+        if (e != hipSuccess && err == hipSuccess) err = e;
+        return false;                     // cancelled: the record goes
+    });
+    if (cur >= 0) (void)hipSetDevice(cur);
+    return err;
+}
+
+void forget_pool_launches(const uint32_t* cancel) {
+    std::lock_guard<std::mutex> g(g_launch_mu);
+    prune_launches([&](const PoolLaunch& l) { return l.cancel != cancel && !launch_done(l); });
+}
+
 static int device_cus() {
     static std::atomic<int> cus[64];       // 0: not yet read (racing readers store the same value)
     int dev = 0;
@@ -790,10 +878,8 @@ static int device_cus() {
 }
 
 template <class R, int ACC>
-static void launch_pool_kernel(const TraceArgs<R>& a0, bool count, double* part, int tiles, int chunks, int chunk,
-                               hipStream_t stream) {
-    TraceArgs<R> a = a0;
-    if (a.im.order_chunk0 < 0) a.im.order_chunk0 = chunks - 1;   // the tile order for the last chunk only
+static hipError_t launch_pool_kernel(const TraceArgs<R>& a, bool count, double* part, int tiles, int chunks,
+                                     int chunk, hipStream_t stream) {
     if constexpr (ACC == ACC_BVH_SPHERES || ACC == ACC_GRID) {
         constexpr int LACC = ACC == ACC_GRID ? ACC_GRID_LDS : ACC_BVH_SPHERES_LDS;
         const size_t lb = ACC == ACC_GRID ? lds_grid_bytes(a.sc) : lds_nodes_bytes(a.sc);
@@ -803,13 +889,13 @@ static void launch_pool_kernel(const TraceArgs<R>& a0, bool count, double* part,
             constexpr int W = lds_waves<R, LACC>();
             const int resident = device_cus() * 4 * waves_per_simd<R, LACC>() / W;
             const int grid = (int)std::min<long long>(resident, (items + W - 1) / W);
-#define RT_LDS_LAUNCH(C, X) hipLaunchKernelGGL((trace_pool_lds_kernel<R, C, LACC, X>), dim3(grid), dim3(64 * W), lb, stream, \
-                                            a, part, tiles, chunk, (int)items, qi)
-            if (a.c.cancel) { if (count) RT_LDS_LAUNCH(true, true); else RT_LDS_LAUNCH(false, true); }
-            else if (count) RT_LDS_LAUNCH(true, false);
-            else RT_LDS_LAUNCH(false, false);
-#undef RT_LDS_LAUNCH
-            return;
+            if (count) hipLaunchKernelGGL((trace_pool_lds_kernel<R, true, LACC>), dim3(grid), dim3(64 * W), lb, stream,
+                                          a, part, tiles, chunk, (int)items, qi);
+            else hipLaunchKernelGGL((trace_pool_lds_kernel<R, false, LACC>), dim3(grid), dim3(64 * W), lb, stream,
+                                    a, part, tiles, chunk, (int)items, qi);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess || !a.c.cancel) return e;
+            return register_pool_launch(a.c, qi, (uint32_t)items, stream);
         }
     }
     const size_t lds = pool_lds_bytes<ACC>(a.sc);
@@ -819,6 +905,7 @@ static void launch_pool_kernel(const TraceArgs<R>& a0, bool count, double* part,
     else if (count) RT_POOL_LAUNCH(true, false);
     else RT_POOL_LAUNCH(false, false);
 #undef RT_POOL_LAUNCH
+    return hipGetLastError();
 }
 
 template <class R, int ACC>
@@ -845,7 +932,7 @@ static hipError_t launch_pool(const TraceArgs<R>& a0, bool count, hipStream_t st
         const int ns = a.im.s_end - b, chunks = (ns + chunk - 1) / chunk;
         if ((long long)tiles * chunks > 0x7FFFFFFFLL) return hipErrorInvalidConfiguration;
         double* part = chunks > 1 ? a0.c.part : nullptr;
-        launch_pool_kernel<R, ACC>(a, count, part, tiles, chunks, chunk, stream);
+        if (const hipError_t e = launch_pool_kernel<R, ACC>(a, count, part, tiles, chunks, chunk, stream)) return e;
         if (part)
             hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)tiles), dim3(64), 0, stream, a.im, a.c.sum,
                                (const double*)part, tiles, chunks, (const uint32_t*)nullptr);
@@ -919,8 +1006,7 @@ template <class R, int ACC>
 static hipError_t launch_partials_acc(const TraceArgs<R>& a, bool count, const PoolPlan& p, double* part,
                                       hipStream_t stream) {
     if ((long long)p.tiles * p.chunks > 0x7FFFFFFFLL) return hipErrorInvalidConfiguration;
-    launch_pool_kernel<R, ACC>(a, count, part, p.tiles, p.chunks, p.chunk, stream);
-    return hipGetLastError();
+    return launch_pool_kernel<R, ACC>(a, count, part, p.tiles, p.chunks, p.chunk, stream);
 }
 
 template <class R>
@@ -958,8 +1044,7 @@ hipError_t launch_trace_batches(const SceneView<R>& sc, const ImageParams& im0, 
     if (im0.cw <= 0 || im0.ch <= 0 || im0.s_end <= im0.s_begin || batch <= 0) return hipSuccess;
     const bool tri = sc.num_tri_nodes > 0;
     const PoolPlan p = pool_plan(im0.cw, im0.ch, batch, tri, im0.pool_chunk);   // one batch's chunks
-    const int stride = im0.batch_stride > 0 ? im0.batch_stride : batch;
-    if (stride < batch) return hipErrorInvalidValue;
+    const int stride = batch * (im0.batch_ways > 1 ? im0.batch_ways : 1);
     const int nb = (im0.s_end - im0.s_begin + stride - 1) / stride;
     if (!part || !c.batch_count || !c.batch_flag || part_bytes < (size_t)nb * p.part_bytes) return hipErrorInvalidValue;
     if ((long long)p.tiles * p.chunks * nb > 0x7FFFFFFFLL) return hipErrorInvalidConfiguration;

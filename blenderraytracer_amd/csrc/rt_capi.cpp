@@ -202,9 +202,6 @@ struct DeviceState {
     DevBuf<double> fused_part;
     DevBuf<uint32_t> fused_count;
     hipEvent_t fused_done = nullptr;
-    // the pool's longest-first tile order of the last crop (tile_order) and that crop's key
-    DevBuf<int> tile_order;
-    int order_key[6] = {-1, -1, -1, -1, -1, -1};
 
     int init(int dev, const HostScene& hs, const rt_scene_desc& d) {
         device = dev;
@@ -240,7 +237,7 @@ struct DeviceState {
         s64.release();
         s32.release();
         sum.release(); segs.release(); draws.release(); total.release(); part.release(); gate_skip.release();
-        fused_part.release(); fused_count.release(); tile_order.release();
+        fused_part.release(); fused_count.release();
         for (DevBuf<double>& b : part_more) b.release();
         for (hipEvent_t e : {ev[0], ev[1], setup_ev, scratch_ev, copy_ev, fused_done})
             if (e) (void)hipEventDestroy(e);
@@ -418,58 +415,6 @@ int check_accel(const rt_scene* sc, const rt_settings* s) {
         return fail(RT_ERR_INVALID, "BVH deeper than the %d-entry traversal stack (too many primitives): use "
                     "RT_ACCEL_AUTO or RT_ACCEL_BRUTE", RT_BVH_STACK);
     return RT_OK;
-}
-
-// The pool's longest-first tile order (pool_order.h item_at): a launch's items taken in raster order end
-// on whatever tiles come last, and its waves drain over the longest of them — config 3's 64-spp share
-// of 8 GPUs measured 6 % below the full frame's rate.  The crop's tiles sorted by the estimated cost of
-// their region (estimate_costs, scene_pack.h), most expensive first (ragged tiles scaled by their pixel
-// count, ties in raster order), so that each chunk of the launch ends on its cheapest tiles.  Only the
-// visiting order changes: the same items, partials and sums.  RT_TILE_LPT (A/B): 0 never (default: on
-// config 3 the order measured 1.6 % slower at 64 spp per rank and 0.3 % at 512 spp, DESIGN.md §4 — the
-// in-flight items lose their screen locality), 1 scenes walked through the grid (the LDS pool kernel's
-// device-wide queue), 2 every BVH scene, 3 grid scenes and only the launch's last chunk (the tail).
-int tile_order_mode() {
-    static const int v = [] {
-        const char* e = getenv("RT_TILE_LPT");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-
-std::vector<int> tile_order_host(const HostScene& hs, const ImageParams& im) {
-    const int tx = (im.cw + 7) / 8, ty = (im.ch + 7) / 8;
-    std::vector<float> cost((size_t)tx * ty);
-    for (int t = 0; t < tx * ty; ++t) {
-        const int x0 = (t % tx) * 8, y0 = (t / tx) * 8;
-        const int vw = std::min(8, im.cw - x0), vh = std::min(8, im.ch - y0);
-        const double X = im.x0 + x0 + 0.5 * vw, Y = im.y0 + y0 + 0.5 * vh;      // tile centre, top-down rows
-        const int i = std::min(kCostNX - 1, (int)(X * kCostNX / im.width));
-        const int r = std::min(kCostNY - 1, (int)(Y * kCostNY / im.height));
-        cost[t] = hs.cost[(size_t)r * kCostNX + i] * (float)(vw * vh);
-    }
-    std::vector<int> order(cost.size());
-    for (size_t t = 0; t < order.size(); ++t) order[t] = (int)t;
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
-    return order;
-}
-
-hipError_t scratch_idle(DeviceState& ds);
-
-// the device copy of the order for this crop (nullptr: raster order), re-uploaded when the crop changes
-const int* tile_order(const rt_scene* sc, DeviceState& ds, const ImageParams& im) {
-    if (sc->hs.cost.empty() || im.cw <= 0 || im.ch <= 0) return nullptr;
-    const int key[6] = {im.width, im.height, im.x0, im.y0, im.cw, im.ch};
-    if (ds.tile_order.p && std::equal(key, key + 6, ds.order_key)) return ds.tile_order.p;
-    const std::vector<int> order = tile_order_host(sc->hs, im);
-    if (scratch_idle(ds) != hipSuccess || ds.tile_order.ensure(order.size()) != hipSuccess ||
-        hipMemcpy(ds.tile_order.p, order.data(), order.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipGetLastError();
-        std::fill(ds.order_key, ds.order_key + 6, -1);
-        return nullptr;                              // raster order: slower only
-    }
-    std::copy(key, key + 6, ds.order_key);
-    return ds.tile_order.p;
 }
 
 // rt_settings.sum_order: the sample pool unless the caller asks for sample order (or RT_SAMPLE_POOL=0)
@@ -804,8 +749,6 @@ int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out) {
     }
     build_bvhs(sc->hs);
     choose_walk(sc->hs, *desc);
-    if (tile_order_mode() == 2 || ((tile_order_mode() == 1 || tile_order_mode() == 3) && sc->hs.use_grid))
-        estimate_costs(sc->hs, *desc);
     sc->desc.set(*desc);
     sc->num_prims = sc->hs.num_prims;
     sc->bvh_prims = (int)(sc->hs.sphere_r.size() + sc->hs.tri_mat.size());
@@ -857,7 +800,10 @@ void rt_scene_destroy(rt_scene* sc) {
 int rt_cancel(rt_scene* sc) {
     if (!sc) return fail(RT_ERR_INVALID, "scene is NULL");
     sc->cancel.store(1);
-    if (sc->ctl) ctl_cancel(sc->ctl, 1);   // the queued batches stop at their next item
+    if (sc->ctl) {
+        ctl_cancel(sc->ctl, 1);             // the one-wave pool kernels skip their items from here on
+        (void)cancel_pool_launches(sc->ctl_dev + kCtlCancel);   // the LDS pool launches' queues end
+    }
     return RT_OK;
 }
 
@@ -937,15 +883,15 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     if ((rc = shard_states(sc, s, states))) return rc;
     sc->cancel.store(0);
     ctl_cancel(sc->ctl, 0);
+    // this render's LDS pool launches are registered under its cancel word until it returns
+    struct LaunchScope {
+        const uint32_t* word;
+        ~LaunchScope() { forget_pool_launches(word); }
+    } launch_scope{sc->ctl_dev + kCtlCancel};
     const size_t n = (size_t)cw * ch;
     const bool want_segs = out && out->segments, want_draws = out && out->draws;
     const bool pool = use_pool(s);
     ImageParams im = image_params(s, cw, ch);
-    if (pool && states.size() == 1 && states[0] == &sc->home) {   // one device: the longest-first tile order
-        HIP_TRY(hipSetDevice(sc->home.device));
-        im.tile_order = tile_order(sc, sc->home, im);
-        im.order_chunk0 = tile_order_mode() == 3 ? -1 : 0;
-    }
     const int base = im.s_begin;                  // the sums hold samples [base, done) of every pixel
     im.s_begin = std::max(im.s_begin, first);
     const int s0 = im.s_begin, s1 = std::max(im.s_end, s0);
@@ -1034,7 +980,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     // drained for 3.5 % of the trace time).  The reduces (16 VGPRs) and the preview frames (gamma
     // thresholds, 29 VGPRs) run beside the trace waves, which leave 32 of a SIMD's 512 VGPRs free.
     // Several devices (the whole-batch split): device d traces its batches k = d, d + N, ... in one launch
-    // (ImageParams::batch_stride), raising batch k's flag; the host then copies that batch's partials to
+    // (ImageParams::batch_ways), raising batch k's flag; the host then copies that batch's partials to
     // the home device and reduces them there in batch order — the copies and reduces of trace_replica,
     // from one launch per device instead of one per batch.
     int fchunk = 0;
@@ -1170,14 +1116,12 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
                     Counters c = with_cancel(cs[e]);
                     c.aborted = sc->ctl_dev + kCtlFusedAborted + 1;   // written by skipping waves, read by no gate
                     c.batch_count = de.fused_count.p;
-                    c.batch_flag = sc->ctl_dev + kCtlFlag + e;
-                    c.flag_stride = nsh;
+                    c.batch_flag = sc->ctl_dev + kCtlFlag + e;          // batch k = e + lb * nsh
                     ImageParams fi = im;
                     fi.s_begin = s0 + e * batch;
                     fi.s_end = s1;
                     fi.pool_chunk = fchunk;
-                    fi.batch_stride = nsh * batch;
-                    if (&de != &h) fi.tile_order = nullptr;   // (set for the home device's launches only)
+                    fi.batch_ways = nsh;
                     const size_t fb = de.fused_part.n * sizeof(double);
                     HIP_TRY(s->precision == RT_PREC_F32
                                 ? launch_trace_batches<float>(de.s32.view, fi, c, bvh, batch, de.fused_part.p, fb, de.tstream[0])
@@ -1191,7 +1135,11 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
             // the host waits for batch kb's flag; without it (a cancel: its items stay untraced) the
             // consumer stream waits for the device's launch to end, so the gate reads the final words
             for (;;) {
-                if (ctl_load(sc->ctl, kCtlFlag + kb) || sc->cancel.load()) break;
+                if (ctl_load(sc->ctl, kCtlFlag + kb)) break;
+                if (sc->cancel.load()) {          // (launches registered after rt_cancel's call, too)
+                    (void)cancel_pool_launches(sc->ctl_dev + kCtlCancel);
+                    break;
+                }
                 const hipError_t q = hipEventQuery(ds.fused_done);
                 if (q == hipSuccess) break;
                 if (q != hipErrorNotReady) {      // a device fault, not a cancel: fail with the HIP error
@@ -1311,6 +1259,7 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
                 // the queued batches stop at their next item and are not reduced; once every stream has
                 // drained, the sums hold exactly the batches the gates committed
                 ctl_cancel(sc->ctl, 1);
+                (void)cancel_pool_launches(sc->ctl_dev + kCtlCancel);
                 for (DeviceState* ds : states) ds->sync_all();
                 h.sync_all();
                 sc->ckpt_done = (int)ctl_load(sc->ctl, kCtlDone);
@@ -1471,10 +1420,6 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
     hipStream_t st = (hipStream_t)hip_stream;
     HIP_TRY(ds.total.ensure(kTotalSlots));
     ImageParams im = image_params(s, cw, ch);
-    if (use_pool(s)) {
-        im.tile_order = tile_order(sc, ds, im);
-        im.order_chunk0 = tile_order_mode() == 3 ? -1 : 0;
-    }
     Counters c{d_sum, nullptr, nullptr, ds.total.p};
     if (s->max_depth > 0 && (rc = ensure_partials(sc, ds, cw, ch, im.s_end - im.s_begin, use_pool(s), c))) return rc;
     HIP_TRY(order_scratch(ds, st));

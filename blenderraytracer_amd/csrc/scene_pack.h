@@ -31,7 +31,6 @@ struct HostScene {   // precision-independent staging, binary64 as packed by the
     int grid_n[3] = {0, 0, 0};
     float grid_lo[3] = {0, 0, 0}, grid_hi[3] = {0, 0, 0}, grid_cs[3] = {1, 1, 1}, grid_far = 0;
     bool use_grid = false;                                        // choose_walk(): the grid walks cheaper
-    std::vector<float> cost;                                      // estimate_costs(): kCostNX x kCostNY, top row first
     int bvh_depth = 0;                                            // deepest leaf of either tree
     int num_prims = 0;
     double record_bytes = 0;      // SURVEY §8d canonical bytes tested per segment
@@ -696,7 +695,7 @@ inline uint32_t host_seed_mix(uint32_t seed) {
 #ifndef RT_GRID_CHOICE
 #define RT_GRID_CHOICE 0.8
 #endif
-// A binary64 SceneView over host copies of the records (the host walks of choose_walk / estimate_costs)
+// A binary64 SceneView over host copies of the records (the host walks of choose_walk)
 inline SceneView<double> host_view(const HostScene& hs, const rt_scene_desc& d, HostRecords<double>& rec) {
     make_records(hs, d, rec);
     SceneView<double> v{};
@@ -749,45 +748,6 @@ inline void choose_walk(HostScene& hs, const rt_scene_desc& d) {
     if (getenv("RT_WALK_DEBUG"))
         fprintf(stderr, "[rt] walk choice: tree %.3g, grid %.3g (%d x %d x %d cells) -> %s\n", tree, grid, hs.grid_n[0],
                 hs.grid_n[1], hs.grid_n[2], hs.use_grid ? "grid" : "tree");
-}
-
-// Estimated cost of the frame's regions (the pool's longest-first tile order, rt_capi.cpp tile_order): a
-// kCostNX x kCostNY raster of pixel-centre camera rays (no lens offset), each followed for up to three
-// segments (a random direction from every hit, as choose_walk) through the walk the trace kernel runs
-// (the kernel's own code on the host), costed as nodes or cells + 0.5 per sphere and 1.5 per triangle
-// test + 4 per segment (shading).  Only the order of the pool's items depends on it, never a result.
-constexpr int kCostNX = 96, kCostNY = 54;
-inline void estimate_costs(HostScene& hs, const rt_scene_desc& d) {
-    hs.cost.clear();
-    if (hs.bvh_depth > 64 || (hs.sphere_r.empty() && hs.tri_mat.empty())) return;
-    HostRecords<double> rec;
-    const SceneView<double> v = host_view(hs, d, rec);
-    const rt_camera_desc& c = d.camera;
-    int stack[64];
-    const BvhStack stk{stack, 1};
-    uint32_t rng = 0x2545F491u;
-    auto uni = [&]() { rng = rng * 1664525u + 1013904223u; return (double)(rng >> 8) * 0x1p-24 * 2.0 - 1.0; };
-    hs.cost.assign((size_t)kCostNX * kCostNY, 0.0f);
-    for (int row = 0; row < kCostNY; ++row)
-        for (int i = 0; i < kCostNX; ++i) {
-            const double u = (i + 0.5) / kCostNX, w = 1.0 - (row + 0.5) / kCostNY;
-            V3<double> o{c.origin[0], c.origin[1], c.origin[2]};
-            V3<double> dir{c.lower_left[0] + u * c.horizontal[0] + w * c.vertical[0] - o.x,
-                           c.lower_left[1] + u * c.horizontal[1] + w * c.vertical[1] - o.y,
-                           c.lower_left[2] + u * c.horizontal[2] + w * c.vertical[2] - o.z};
-            double cost = 0;
-            for (int seg = 0; seg < 3; ++seg) {
-                Work wk{};
-                const Closest<double> h = hs.use_grid ? closest_hit_grid<double>(v, o, dir, wk, stk)
-                                        : hs.tri_mat.empty() ? closest_hit_bvh<double, true, false>(v, o, dir, wk, stk)
-                                                             : closest_hit_bvh<double, true, true>(v, o, dir, wk, stk);
-                cost += wk.nodes + 0.5 * wk.spheres + 1.5 * wk.tris + 4.0;
-                if (h.kind == HIT_NONE) break;
-                o = o + dir * h.t;
-                dir = V3<double>{uni(), uni(), uni()};
-            }
-            hs.cost[(size_t)row * kCostNX + i] = (float)cost;
-        }
 }
 
 }  // namespace rt

@@ -393,6 +393,18 @@ extern "C" void ptc_chunk_range(int s_begin, int s_end, int batch_samples, int b
     const ChunkRange r = chunk_range(im, gci, chunk);
     out[0] = r.b; out[1] = r.ci; out[2] = r.sb; out[3] = r.se;
 }
+// ... of a device's launch in the whole-batch split (ImageParams::batch_ways)
+extern "C" void ptc_chunk_range_ways(int s_begin, int s_end, int batch_samples, int batch_chunks, int ways, int gci,
+                                     int chunk, int* out) {
+    ImageParams im{};
+    im.s_begin = s_begin;
+    im.s_end = s_end;
+    im.batch_samples = batch_samples;
+    im.batch_chunks = batch_chunks;
+    im.batch_ways = ways;
+    const ChunkRange r = chunk_range(im, gci, chunk);
+    out[0] = r.b; out[1] = r.ci; out[2] = r.sb; out[3] = r.se;
+}
 
 // root_div (pt_core.h RT_ROOT_RCP, TEST TOOL): x / a through RN(1 / a) and a Markstein correction
 extern "C" void ptc_root_div(const double* x, const double* a, double* out, long long n) {

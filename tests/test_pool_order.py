@@ -88,3 +88,34 @@ def test_fused_chunks_are_the_batches_chunks(s0, s1, batch, chunk):
         else:
             assert se <= sb, (gci, sb, se)                          # a short last batch's missing chunk
     assert seen == list(range(s0, s1))                               # every sample once, in order
+
+
+@pytest.mark.parametrize("s0,s1,batch,chunk,ways", [(0, 512, 32, 32, 2), (0, 512, 32, 11, 8), (0, 24, 3, 3, 3),
+                                                    (5, 17, 4, 3, 2), (0, 100, 7, 3, 3), (0, 1000, 64, 45, 8)])
+def test_multi_device_fused_chunks_are_the_batches_chunks(s0, s1, batch, chunk, ways):
+    """The whole-batch multi-device split with fused launches: device d's launch (s_begin = s0 + d batch,
+    ImageParams::batch_ways = N) gives its local batch lb the samples and chunks of the render's batch
+    k = d + lb N as that batch's own launch has them, so every sample is traced once, by one device, in
+    the same chunks as on one device (bit-identical sums after the batch-order reduces)."""
+    import ctypes as C
+    L = hc.lib()
+    L.ptc_chunk_range.argtypes = [C.c_int] * 6 + [C.POINTER(C.c_int)]
+    L.ptc_chunk_range_ways.argtypes = [C.c_int] * 7 + [C.POINTER(C.c_int)]
+    nb = -(-(s1 - s0) // batch)
+    chunks_b = -(-batch // chunk)
+    seen = []
+    for d in range(ways):
+        nbd = -(-(nb - d) // ways) if nb > d else 0
+        for gci in range(nbd * chunks_b):
+            out = (C.c_int * 4)()
+            L.ptc_chunk_range_ways(s0 + d * batch, s1, batch, chunks_b, ways, gci, chunk, out)
+            lb, ci, sb, se = tuple(out)
+            k = d + lb * ways
+            bb, be = s0 + k * batch, min(s1, s0 + (k + 1) * batch)
+            if ci < -(-(be - bb) // chunk):
+                assert (sb, se) == _chunk_range(L, bb, be, 0, 0, ci, chunk)[2:], (d, gci)
+                seen.extend(range(sb, se))
+            else:
+                assert se <= sb
+    assert sorted(seen) == list(range(s0, s1))
+
