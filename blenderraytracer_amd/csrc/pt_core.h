@@ -116,17 +116,50 @@ template <class R> RT_HD bool div_rcp_range(R x) {
     const R ax = fabs(x);
     return ax >= (R)(sizeof(R) == 8 ? 0x1p-500 : 0x1p-60) && ax <= (R)(sizeof(R) == 8 ? 0x1p500 : 0x1p60);
 }
+// smallest / largest |a.k| (device: IEEE minimum / maximum, NaN-propagating — a NaN fails every guard
+// compare; host: fmin / fmax, where a NaN component goes through div_rcp_1 and stays NaN)
+template <class R> RT_HD R min3abs(V3<R> a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_elementwise_minimum(fabs(a.x), __builtin_elementwise_minimum(fabs(a.y), fabs(a.z)));
+#else
+    return fmin(fabs(a.x), fmin(fabs(a.y), fabs(a.z)));
+#endif
+}
+template <class R> RT_HD R max3abs(V3<R> a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_elementwise_maximum(fabs(a.x), __builtin_elementwise_maximum(fabs(a.y), fabs(a.z)));
+#else
+    return fmax(fabs(a.x), fmax(fabs(a.y), fabs(a.z)));
+#endif
+}
 template <class R> RT_HD V3<R> vdiv_rcp(V3<R> a, R s, R y) {
     const R smin = sizeof(R) == 8 ? (R)0x1p-400 : (R)0x1p-40, smax = sizeof(R) == 8 ? (R)0x1p400 : (R)0x1p40;
+    const R xmin = sizeof(R) == 8 ? (R)0x1p-500 : (R)0x1p-60, xmax = sizeof(R) == 8 ? (R)0x1p500 : (R)0x1p60;
     const R as = fabs(s);
-    if (div_rcp_on<R>() && div_rcp_range(a.x) && div_rcp_range(a.y) && div_rcp_range(a.z) && as >= smin && as <= smax)
+    // every component in div_rcp_range, as one min3 and one max3 (RTOW f32: six compares fewer)
+    if (div_rcp_on<R>() && min3abs(a) >= xmin && max3abs(a) <= xmax && as >= smin && as <= smax)
         return {div_rcp_1(a.x, s, y), div_rcp_1(a.y, s, y), div_rcp_1(a.z, s, y)};
     return vdiv(a, s);
+}
+// normalize's a / l, l = RN(sqrt(RN(RN(ax^2 + ay^2) + az^2))): every |a.k| <= l (1 + 2^-22) (three
+// roundings of the sum, one of the sqrt; an overflowing square makes l infinite), so the quotients lie
+// within the guard's range once l does and the smallest |a.k| does — one min3 and three compares
+// instead of vdiv_rcp's nine (RT_UNIT_GUARD=0, A/B: vdiv_rcp's guard)
+#ifndef RT_UNIT_GUARD
+#define RT_UNIT_GUARD 1
+#endif
+template <class R> RT_HD V3<R> vdiv_rcp_unit(V3<R> a, R l, R y) {
+    if (!RT_UNIT_GUARD) return vdiv_rcp(a, l, y);
+    const R smin = sizeof(R) == 8 ? (R)0x1p-400 : (R)0x1p-40, smax = sizeof(R) == 8 ? (R)0x1p400 : (R)0x1p40;
+    const R xmin = sizeof(R) == 8 ? (R)0x1p-500 : (R)0x1p-60;
+    if (div_rcp_on<R>() && min3abs(a) >= xmin && l >= smin && l <= smax)
+        return {div_rcp_1(a.x, l, y), div_rcp_1(a.y, l, y), div_rcp_1(a.z, l, y)};
+    return vdiv(a, l);
 }
 template <class R> RT_HD V3<R> normalize(V3<R> a) {          // math.js:18
     R l = sqrt(a.x * a.x + a.y * a.y + a.z * a.z);
 #if RT_DIV_RCP
-    return l > (R)0 ? vdiv_rcp(a, l, (R)1 / l) : mk<R>(0, 0, 0);
+    return l > (R)0 ? vdiv_rcp_unit(a, l, (R)1 / l) : mk<R>(0, 0, 0);
 #else
     return l > (R)0 ? vdiv(a, l) : mk<R>(0, 0, 0);
 #endif
@@ -260,10 +293,10 @@ struct Closest { R t; int kind, idx, mat, obj; };   // obj: World.objects index 
 #define RT_LEAVE_ALL 0
 #endif
 #ifndef RT_LEAVE_INSIDE
-#define RT_LEAVE_INSIDE 1         // 0 (A/B): round 4's away rule only (c >= 0)
+#define RT_LEAVE_INSIDE 1         // binary64 only (binary32 measured -0.7 %); 2 (A/B): both; 0 (A/B): round 4's away rule only
 #endif
 template <class R> RT_HD bool sphere_leaves(R hb, R c, R a, R tmin) {
-    if (!RT_LEAVE_INSIDE) return hb >= (R)0 && c >= (R)0;
+    if (!RT_LEAVE_INSIDE || (sizeof(R) == 4 && RT_LEAVE_INSIDE == 1)) return hb >= (R)0 && c >= (R)0;
     return hb >= (R)0 &&
            (c >= (R)0 || (-c < hb * (tmin * (R)0.25) && hb * (R)(sizeof(R) == 8 ? 0x1p-45 : 0x1p-18) < a * (tmin * (R)0.25)));
 }

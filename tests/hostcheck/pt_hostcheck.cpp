@@ -440,6 +440,31 @@ extern "C" void ptc_div_rcp_f64(const double* x, const double* s, double* out2, 
     }
 }
 
+// normalize<float> (vdiv_rcp_unit: the min3 guard) against three IEEE divisions by the same l, bit for
+// bit, on vectors whose components spread over 2^-149 .. 2^70 (zeros, subnormals, overflowing squares
+// and mixed magnitudes included).  Returns the number of mismatching components (NaN == NaN).
+extern "C" long long ptc_normalize_check(long long n, unsigned seed) {
+    std::mt19937_64 gen(seed);
+    std::uniform_real_distribution<double> U(0.0, 1.0);
+    long long bad = 0;
+    auto comp = [&]() -> float {
+        const int kind = (int)(gen() % 10);
+        if (kind == 0) return 0.0f;
+        const double e = kind == 1 ? -149 + 30 * U(gen) : kind == 2 ? 40 + 30 * U(gen) : -70 + 100 * U(gen);
+        const float v = (float)(std::ldexp(1.0 + U(gen), (int)std::floor(e)));
+        return (gen() & 1) ? -v : v;
+    };
+    for (long long i = 0; i < n; ++i) {
+        const rt::V3<float> a{comp(), comp(), comp()};
+        const rt::V3<float> q = rt::normalize<float>(a);
+        const float l = std::sqrt(a.x * a.x + a.y * a.y + a.z * a.z);
+        const rt::V3<float> r = l > 0.0f ? rt::vdiv<float>(a, l) : rt::V3<float>{0, 0, 0};
+        auto same = [](float u, float v) { return (u != u && v != v) || memcmp(&u, &v, 4) == 0; };
+        bad += !same(q.x, r.x) + !same(q.y, r.y) + !same(q.z, r.z);
+    }
+    return bad;
+}
+
 // Adversarial check of the binary32 triangle pre-filter (pt_core.h tri_filter_pass, tri_filter_bound):
 // random triangles over 7 decades of scale and shape (slivers included), rays through points at
 // barycentric distance 10^-1 .. 10^-12 from an edge or a vertex (inside and outside), rays whose A = d.n

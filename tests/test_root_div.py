@@ -106,3 +106,13 @@ def test_vdiv_rcp_f32_every_significand():
     L.ptc_div_rcp_f32_exhaustive.argtypes = [C.c_int, C.c_uint]
     L.ptc_div_rcp_f32_exhaustive.restype = C.c_longlong
     assert L.ptc_div_rcp_f32_exhaustive(80, 99) == 0
+
+
+def test_normalize_unit_guard_f32():
+    """normalize<float> through vdiv_rcp_unit (one min3 + three compares as the guard, pt_core.h) equals
+    three IEEE divisions by the same length, bit for bit, on 2 M vectors whose components mix zeros,
+    subnormals, squares that overflow and magnitudes 2^-149 .. 2^70."""
+    L = hc.lib()
+    L.ptc_normalize_check.argtypes = [C.c_longlong, C.c_uint]
+    L.ptc_normalize_check.restype = C.c_longlong
+    assert L.ptc_normalize_check(2_000_000, 7) == 0
