@@ -270,8 +270,8 @@ struct SceneView {
     int num_grid_recs;             // grid_cell[num_grid_cells]: registrations (records in grid_leaf)
     int use_grid;                  // choose_walk (scene_pack.h): the trace kernel walks the grid
     // camera (camera.js:8-36 vectors, computed on the host in binary64)
-    R cam_o[3], cam_llc[3], cam_h[3], cam_v[3], cam_u[3], cam_vv[3], cam_w[3];
-    R lens_radius;
+    R cam_o[3], cam_llc[3], cam_h[3], cam_v[3], cam_u[3], cam_vv[3], cam_w[3];   // contiguous with
+    R lens_radius;                                                                 // lens_radius: start_sample
     int cam_ortho;
     int background;
     R sky_intensity;

@@ -47,7 +47,35 @@ RT_COLD_HD AaUv<R> stochastic_uv(uint32_t key, int i, int j, int width, int heig
 #ifndef RT_OPAQUE_WH
 #define RT_OPAQUE_WH 0
 #endif
-template <class R>
+// The camera ray (camera.js:38-51) from the camera's 22 words at cp (SceneView: cam_o, cam_llc, cam_h,
+// cam_v, cam_u, cam_vv, cam_w, lens_radius, contiguous)
+template <class R, class P>
+RT_HD void camera_ray(const SceneView<R>& sc, R u, R v, Rng<R>& g, V3<R>& o, V3<R>& d, P cp) {
+    const V3<R> co = mk<R>(cp[0], cp[1], cp[2]);
+    const V3<R> llc = mk<R>(cp[3], cp[4], cp[5]);
+    const V3<R> hor = mk<R>(cp[6], cp[7], cp[8]);
+    const V3<R> ver = mk<R>(cp[9], cp[10], cp[11]);
+    const V3<R> cu = mk<R>(cp[12], cp[13], cp[14]);
+    const V3<R> cv = mk<R>(cp[15], cp[16], cp[17]);
+    V3<R> rd = random_in_unit_disk(g) * (R)cp[21];
+    if (sc.cam_ortho) {
+        o = (co + cu * rd.x) + cv * rd.y;
+        d = normalize((((llc + hor * u) + ver * v) - o) + mk<R>(cp[18], cp[19], cp[20]) * (R)-1);
+    } else {
+        o = co + (cu * rd.x + cv * rd.y);
+        d = ((llc + hor * u) + ver * v) - o;
+    }
+}
+
+// RELOAD (RT_CAM_RELOAD: the binary32 LDS pool kernel): the camera words read from the kernel-argument
+// segment at every sample start (scalar loads through a pointer the compiler cannot hoist) instead of
+// kept live in SGPRs across the segment loop, where the kernel's SGPR spills are reloaded by VALU
+// v_readlane instructions: RTOW f32 +1.6 % (SGPR spills 61 -> 49).  In binary64 the freed SGPRs went to
+// spills inside the walk instead (RTOW -0.3 %, mesh50k -9 %, Cornell -16 %), so binary32 only.
+#ifndef RT_CAM_RELOAD
+#define RT_CAM_RELOAD 1
+#endif
+template <class R, bool RELOAD = false>
 RT_HD void start_sample(const SceneView<R>& sc, const ImageParams& im, int i, int j, uint32_t pkey, int s, Rng<R>& g,
                         V3<R>& o, V3<R>& d) {
     RT_HCOUNT(HC_SAMPLES, 1);
@@ -75,20 +103,20 @@ RT_HD void start_sample(const SceneView<R>& sc, const ImageParams& im, int i, in
         u = ((R)i + (R)0.5) / width;
         v = ((R)j + (R)0.5) / height;
     }
-    const V3<R> cu = mk(sc.cam_u[0], sc.cam_u[1], sc.cam_u[2]);               // camera.js:38-51
-    const V3<R> cv = mk(sc.cam_vv[0], sc.cam_vv[1], sc.cam_vv[2]);
-    const V3<R> co = mk(sc.cam_o[0], sc.cam_o[1], sc.cam_o[2]);
-    const V3<R> llc = mk(sc.cam_llc[0], sc.cam_llc[1], sc.cam_llc[2]);
-    const V3<R> hor = mk(sc.cam_h[0], sc.cam_h[1], sc.cam_h[2]);
-    const V3<R> ver = mk(sc.cam_v[0], sc.cam_v[1], sc.cam_v[2]);
-    V3<R> rd = random_in_unit_disk(g) * sc.lens_radius;
-    if (sc.cam_ortho) {
-        o = (co + cu * rd.x) + cv * rd.y;
-        d = normalize((((llc + hor * u) + ver * v) - o) + mk(sc.cam_w[0], sc.cam_w[1], sc.cam_w[2]) * (R)-1);
-    } else {
-        o = co + (cu * rd.x + cv * rd.y);
-        d = ((llc + hor * u) + ver * v) - o;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (RELOAD && RT_CAM_RELOAD != 0) {
+        // sc is the kernel's first argument's first member (the trace kernels take TraceArgs first,
+        // pt_trace.hip): its camera words sit at offsetof(SceneView, cam_o) in the kernel-argument
+        // segment.  (Taking &sc.cam_o instead makes the argument escape into a private copy.)
+        typedef const __attribute__((address_space(4))) R* CamPtr;
+        typedef const __attribute__((address_space(4))) char* ArgPtr;
+        CamPtr cp = (CamPtr)((ArgPtr)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(SceneView<R>, cam_o));
+        asm volatile("" : "+s"(cp));
+        camera_ray(sc, u, v, g, o, d, cp);
+        return;
     }
+#endif
+    camera_ray(sc, u, v, g, o, d, &sc.cam_o[0]);
 }
 
 // x^5 for Schlick's approximation (materials.js:79-83, Math.pow(1 - cosine, 5)), correctly rounded.

@@ -25,10 +25,11 @@ namespace rt {
 
 template <class R>
 struct TraceArgs {
-    SceneView<R> sc;
-    ImageParams im;
-    Counters c;
+    SceneView<R> sc;            // first: start_sample reads the camera at its kernel-argument offset
+    ImageParams im;             // (RT_CAM_RELOAD, pt_path.h), so every trace kernel takes TraceArgs
+    Counters c;                 // as its first argument
 };
+static_assert(offsetof(TraceArgs<double>, sc) == 0 && offsetof(TraceArgs<float>, sc) == 0, "sc first");
 
 // One wave (an 8x8 pixel tile) per workgroup: one-wave workgroups measured fastest (RTOW f64 4350 vs
 // 4190 Msamples/s for 16x16 tiles, mesh50k 3342 vs 3094): finer work items shorten the frame's tail.
@@ -445,7 +446,7 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
         T = mk<R>(1, 1, 1);
         depth = im.max_depth;
         isegs = 0;
-        start_sample(sc, im, i, j, pkey, s, g, o, d);
+        start_sample<R, sizeof(R) == 4>(sc, im, i, j, pkey, s, g, o, d);
     };
     uint32_t next = 64;                       // items [0, 64) are dealt to lanes 0..63 up front
     bool live = (uint32_t)lane < total;
