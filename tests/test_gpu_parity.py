@@ -561,6 +561,63 @@ def test_cancel_latency_within_a_batch(gpu, tmp_path, devices):
     assert bool(r["equal"])
 
 
+_TWO_RENDERS_SCRIPT = r'''
+import sys, threading, time
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+import torch  # noqa: F401  (HIP runtime first)
+from blenderraytracer_amd import capi
+from blenderraytracer_amd.renderer import GpuRayTracer
+from blenderraytracer_amd.scene import load_scene_json
+def tracer(seed):
+    rt = GpuRayTracer(960, 540, seed=seed)
+    assert rt.load_from_json(load_scene_json("rtow.json"))
+    rt.update_render_settings({"maxBounces": 5, "samples": 256})
+    return rt
+a, b = tracer(3), tracer(4)
+ref_a = a.render(want=("mean",), batch_samples=32)["mean"]
+t = time.perf_counter()
+ref_b = b.render(want=("mean",), batch_samples=32)["mean"]
+frame_s = time.perf_counter() - t
+lib = capi.load_library()
+box = {}
+def run(name, rt):
+    try:
+        box[name] = rt.render(want=("mean",), batch_samples=32)["mean"]
+    except RuntimeError as e:
+        box[name] = str(e)
+ta, tb = threading.Thread(target=run, args=("a", a)), threading.Thread(target=run, args=("b", b))
+ta.start(); tb.start()
+time.sleep(0.5 * frame_s)
+capi.check(lib.rt_cancel(a.scene_handle()))
+ta.join(); tb.join()
+sums, done = a.checkpoint()
+res_a = tracer(3).render(want=("mean",), resume=(sums, done), batch_samples=32)["mean"]
+np.savez(sys.argv[2], a_cancelled=isinstance(box["a"], str) and "cancel" in box["a"].lower(),
+         b_equal=(not isinstance(box["b"], str)) and np.array_equal(box["b"], ref_b),
+         a_resume_equal=np.array_equal(res_a, ref_a), done=done)
+'''
+
+
+def test_cancel_one_of_two_concurrent_renders(gpu, tmp_path):
+    """The in-flight launches a cancel moves are those of the cancelled render only (cancel_pool_launches
+    keys them by the scene's cancel word): two progressive renders of two scenes run at once on two
+    threads, one is cancelled mid-frame — the other finishes bit-identical to its own uninterrupted
+    render, and the cancelled one's checkpoint resumes bit-exactly."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", _TWO_RENDERS_SCRIPT, root, str(tmp_path / "t.npz")],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    r = np.load(tmp_path / "t.npz")
+    print(f"cancelled render's checkpoint: {int(r['done'])} samples")
+    assert bool(r["a_cancelled"])
+    assert bool(r["b_equal"])
+    assert bool(r["a_resume_equal"])
+
+
 def test_config4_rtow_4k_1024spp_sharded(gpu):
     """Config 4 at its full size: RTOW 3840x2160 x 1024 spp (8.5e9 samples).  (1) Through
     rt_trace_device, 8 sample-range shards (the per-GPU work of the 8-GPU split, run one after another
