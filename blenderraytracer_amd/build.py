@@ -20,7 +20,11 @@ REPO = os.path.dirname(HERE)
 ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 
-SOURCES = ["pt_trace.hip", "rt_capi.cpp", "scene_json.cpp"]
+SOURCES = ["pt_trace.hip", "pt_onewave.hip", "rt_capi.cpp", "scene_json.cpp"]
+# per-source flags: the one-wave pool and lane-per-pixel kernels (pt_onewave.hip) with LLVM's AMDGPU
+# register-pressure trackers during scheduling (mesh50k +1.0 %, Cornell +1.4 %; the LDS kernels -3.6 %
+# with it, so not for pt_trace.hip)
+SOURCE_FLAGS = {"pt_onewave.hip": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"]}
 # -structurizecfg-skip-uniform-regions: branches the compiler proves wave-uniform stay plain scalar
 # branches instead of exec-mask regions (RTOW +0.9 %, mesh50k +0.5 %, identical images)
 HIP_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
@@ -91,7 +95,7 @@ def build_lib(force=False):
     objs = []
     for src in SOURCES:
         obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
-        _run([HIPCC, *HIP_FLAGS, "-c", os.path.join(CSRC, src), "-o", obj])
+        _run([HIPCC, *HIP_FLAGS, *SOURCE_FLAGS.get(src, []), "-c", os.path.join(CSRC, src), "-o", obj])
         objs.append(obj)
     _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", target, *objs])
     write_build_info()

@@ -516,6 +516,7 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
     __builtin_amdgcn_wave_barrier();
 }
 
+#if !RT_ONEWAVE_TU   // the LDS pool kernels, the reduce and the host API: pt_trace.hip's own translation unit
 // ---- sample pool with the sphere tree's nodes in LDS (ACC_BVH_SPHERES_LDS) ----
 // The walk's divergent node reads (4 x 16 B per lane and step through the vector memory path, which
 // is ~0.86 busy on RTOW) become LDS reads: a workgroup of lds_waves() waves copies the
@@ -693,6 +694,8 @@ static int pool_chunk(int ns, int tiles, bool tri_bvh) {
     return c;
 }
 
+#endif  // !RT_ONEWAVE_TU
+
 // dynamic LDS of a trace launch: the ordered walk's per-lane stacks (the scene's deepest leaf entries)
 template <int ACC, class R>
 static size_t stack_lds_bytes(const SceneView<R>& sc) {
@@ -707,6 +710,53 @@ static size_t pool_lds_bytes(const SceneView<R>& sc) {
 }
 
 static int crop_tiles(int cw, int ch) { return ((cw + 7) / 8) * ((ch + 7) / 8); }
+
+// The one-wave pool kernel (trace_pool_kernel) and the lane-per-pixel kernel (trace_kernel) are
+// compiled in a translation unit of their own, pt_onewave.hip (this file with RT_ONEWAVE_TU), with
+// LLVM's AMDGPU register-pressure trackers (build.py: mesh50k +1.0 %, Cornell +1.4 %; the same flag
+// costs the LDS kernels 3.6 %).  Their kernels are instantiated and launched only there.
+template <class R, int ACC>
+hipError_t launch_onewave_pool(const TraceArgs<R>& a, bool count, double* part, int tiles, int chunks, int chunk,
+                               hipStream_t stream);
+template <class R, int ACC>
+hipError_t launch_lane_kernel(const TraceArgs<R>& a, bool count, hipStream_t stream);
+
+#if RT_ONEWAVE_TU
+template <class R, int ACC>
+hipError_t launch_onewave_pool(const TraceArgs<R>& a, bool count, double* part, int tiles, int chunks, int chunk,
+                               hipStream_t stream) {
+    const size_t lds = pool_lds_bytes<ACC>(a.sc);
+#define RT_POOL_LAUNCH(C, X) hipLaunchKernelGGL((trace_pool_kernel<R, C, ACC, X>), dim3(tiles * chunks), dim3(64), lds, stream, \
+                                             a, part, tiles, chunk)
+    if (a.c.cancel) { if (count) RT_POOL_LAUNCH(true, true); else RT_POOL_LAUNCH(false, true); }
+    else if (count) RT_POOL_LAUNCH(true, false);
+    else RT_POOL_LAUNCH(false, false);
+#undef RT_POOL_LAUNCH
+    return hipGetLastError();
+}
+template <class R, int ACC>
+hipError_t launch_lane_kernel(const TraceArgs<R>& a, bool count, hipStream_t stream) {
+    const int tiles = crop_tiles(a.im.cw, a.im.ch);
+    const size_t lds = stack_lds_bytes<ACC>(a.sc);
+    if (count) hipLaunchKernelGGL((trace_kernel<R, true, ACC>), dim3(tiles), dim3(64), lds, stream, a);
+    else hipLaunchKernelGGL((trace_kernel<R, false, ACC>), dim3(tiles), dim3(64), lds, stream, a);
+    return hipGetLastError();
+}
+#define RT_ONEWAVE_INST(R, ACC)                                                                                  \
+    template hipError_t launch_onewave_pool<R, ACC>(const TraceArgs<R>&, bool, double*, int, int, int, hipStream_t); \
+    template hipError_t launch_lane_kernel<R, ACC>(const TraceArgs<R>&, bool, hipStream_t);
+RT_ONEWAVE_INST(double, ACC_BRUTE)
+RT_ONEWAVE_INST(double, ACC_BVH)
+RT_ONEWAVE_INST(double, ACC_BVH_STACK)
+RT_ONEWAVE_INST(double, ACC_BVH_SPHERES)
+RT_ONEWAVE_INST(double, ACC_GRID)
+RT_ONEWAVE_INST(float, ACC_BRUTE)
+RT_ONEWAVE_INST(float, ACC_BVH)
+RT_ONEWAVE_INST(float, ACC_BVH_STACK)
+RT_ONEWAVE_INST(float, ACC_BVH_SPHERES)
+RT_ONEWAVE_INST(float, ACC_GRID)
+#undef RT_ONEWAVE_INST
+#else   // !RT_ONEWAVE_TU: the rest of the file
 
 size_t pool_partial_bytes(int cw, int ch, int ns, bool tri_bvh, int chunk_override) {
     if (cw <= 0 || ch <= 0 || ns <= 0) return 0;
@@ -899,14 +949,7 @@ static hipError_t launch_pool_kernel(const TraceArgs<R>& a, bool count, double* 
             return register_pool_launch(a.c, qi, (uint32_t)items, stream);
         }
     }
-    const size_t lds = pool_lds_bytes<ACC>(a.sc);
-#define RT_POOL_LAUNCH(C, X) hipLaunchKernelGGL((trace_pool_kernel<R, C, ACC, X>), dim3(tiles * chunks), dim3(64), lds, stream, \
-                                             a, part, tiles, chunk)
-    if (a.c.cancel) { if (count) RT_POOL_LAUNCH(true, true); else RT_POOL_LAUNCH(false, true); }
-    else if (count) RT_POOL_LAUNCH(true, false);
-    else RT_POOL_LAUNCH(false, false);
-#undef RT_POOL_LAUNCH
-    return hipGetLastError();
+    return launch_onewave_pool<R, ACC>(a, count, part, tiles, chunks, chunk, stream);
 }
 
 template <class R, int ACC>
@@ -967,11 +1010,7 @@ template bool trace_walks_grid<float>(const SceneView<float>&);
 template <class R, int ACC>
 static hipError_t launch_acc(const TraceArgs<R>& a, bool count, bool pool, hipStream_t stream) {
     if (pool) return launch_pool<R, ACC>(a, count, stream);
-    const int tiles = crop_tiles(a.im.cw, a.im.ch);
-    const size_t lds = stack_lds_bytes<ACC>(a.sc);
-    if (count) hipLaunchKernelGGL((trace_kernel<R, true, ACC>), dim3(tiles), dim3(64), lds, stream, a);
-    else hipLaunchKernelGGL((trace_kernel<R, false, ACC>), dim3(tiles), dim3(64), lds, stream, a);
-    return hipGetLastError();
+    return launch_lane_kernel<R, ACC>(a, count, stream);
 }
 
 template <class R>
@@ -1353,5 +1392,7 @@ hipError_t launch_denoise(int w, int h, double w1, double w2, const float* in, f
     hipLaunchKernelGGL(denoise_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, w, h, w1, w2, in, out, rgba8);
     return hipGetLastError();
 }
+
+#endif  // !RT_ONEWAVE_TU
 
 }  // namespace rt

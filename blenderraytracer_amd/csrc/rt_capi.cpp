@@ -933,9 +933,11 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     // the pool's rule for the shard's whole share of the render (not for one batch: short chunks lengthen
     // each wave's drain relative to its work), balanced over the shard's part of a full batch.  The same
     // batches give the same chunks on a resume (the share is counted from sample_begin), so a resumed
-    // render stays bit-identical.
+    // render stays bit-identical — also when the resume has a single batch left (the render as a whole,
+    // from sample_begin, has several: before round 5 that batch took the pool's rule for its own
+    // samples, 1-ulp differences in the resumed sums).
     std::vector<int> chunk_hint(nsh, whole ? whole_chunk : 0);
-    if (pool && nb > 1 && !whole)
+    if (pool && !whole && (nb > 1 || (s->batch_samples > 0 && s->batch_samples < s1 - base)))
         for (int k = 0; k < nsh; ++k) {
             int a, b, fa, fb;
             shard_range(base, s1, k, nsh, a, b);

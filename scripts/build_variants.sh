@@ -4,14 +4,15 @@
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/blenderraytracer_amd/lib/variants
-SRCS="pt_trace.hip rt_capi.cpp scene_json.cpp"     # the same sources as blenderraytracer_amd/build.py
+SRCS="pt_trace.hip pt_onewave.hip rt_capi.cpp scene_json.cpp"   # the same sources (and per-source flags) as build.py
 mkdir -p "$OUT"
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   objs=""
   for src in $SRCS; do
     obj="$OUT/$name.${src%.*}.o"
-    /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -mllvm -structurizecfg-skip-uniform-regions=1 $flags -I "$ROOT/include" \
+    extra=""; [ $src = pt_onewave.hip ] && [ -z "$NO_TRK" ] && extra="-mllvm -amdgpu-use-amdgpu-trackers=1"
+    /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -mllvm -structurizecfg-skip-uniform-regions=1 $extra $flags -I "$ROOT/include" \
       -c "$ROOT/blenderraytracer_amd/csrc/$src" -o "$obj" &
     objs="$objs $obj"
   done

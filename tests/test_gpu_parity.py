@@ -254,6 +254,28 @@ def test_bvh_bit_identical_to_brute_mesh50k(gpu, precision):
     rt.close()
 
 
+def test_resume_with_one_batch_left_is_bit_exact(gpu):
+    """A resume whose remaining samples are a single batch (the render as a whole has several) takes
+    that batch's chunks from the whole render's rule, as the uninterrupted render did: bit-identical.
+    (Round 5: the single batch took the pool's rule for its own 32 samples — 11 + 11 + 10 instead of
+    32 — and the resumed sums differed by 1 ulp in most pixels.)  Cancelled from the progress call
+    after the 2nd of 3 fused batches: the checkpoint is 64 samples (or 96 if the 3rd batch finished
+    before the cancel reached it)."""
+    rt = _rtow(640, 360, 96)
+    full = rt.render(want=("mean",), batch_samples=32)
+    calls = []
+    with pytest.raises(RuntimeError, match="CANCELLED"):
+        rt.render(batch_samples=32, on_progress=lambda f: calls.append(f) or len(calls) >= 2)
+    sums, done = rt.checkpoint()
+    rt.close()
+    print(f"checkpoint {done} samples")
+    assert done in (64, 96)
+    rt2 = _rtow(640, 360, 96)
+    res = rt2.render(want=("mean",), resume=(sums, done), batch_samples=32)
+    assert np.array_equal(res["mean"], full["mean"])
+    rt2.close()
+
+
 def test_checkpoint_resume_is_bit_exact(gpu):
     """Progressive rendering: cancel after some batches, checkpoint the float64 sums,
     resume in a NEW scene handle from the saved state: identical bits to an uninterrupted render with
@@ -576,23 +598,29 @@ def tracer(seed):
     return rt
 a, b = tracer(3), tracer(4)
 ref_a = a.render(want=("mean",), batch_samples=32)["mean"]
-t = time.perf_counter()
 ref_b = b.render(want=("mean",), batch_samples=32)["mean"]
-frame_s = time.perf_counter() - t
 lib = capi.load_library()
 box = {}
-def run(name, rt):
+calls = []
+def cancel_a(f):                      # A's 3rd progress call cancels A through rt_cancel, B still running
+    calls.append(f)
+    if len(calls) == 3:
+        capi.check(lib.rt_cancel(a.scene_handle()))
+    return False
+def run(name, rt, cb):
     try:
-        box[name] = rt.render(want=("mean",), batch_samples=32)["mean"]
+        box[name] = rt.render(want=("mean",), batch_samples=32, on_progress=cb)["mean"]
     except RuntimeError as e:
         box[name] = str(e)
-ta, tb = threading.Thread(target=run, args=("a", a)), threading.Thread(target=run, args=("b", b))
-ta.start(); tb.start()
-time.sleep(0.5 * frame_s)
-capi.check(lib.rt_cancel(a.scene_handle()))
+ta = threading.Thread(target=run, args=("a", a, cancel_a))
+tb = threading.Thread(target=run, args=("b", b, None))
+tb.start(); ta.start()
 ta.join(); tb.join()
 sums, done = a.checkpoint()
 res_a = tracer(3).render(want=("mean",), resume=(sums, done), batch_samples=32)["mean"]
+diff = np.abs(res_a - ref_a)
+print("done", done, "a:", box["a"] if isinstance(box["a"], str) else "finished", "resume max|diff|", float(diff.max()),
+      "pixels differing", int(np.count_nonzero(diff)), file=sys.stderr)
 np.savez(sys.argv[2], a_cancelled=isinstance(box["a"], str) and "cancel" in box["a"].lower(),
          b_equal=(not isinstance(box["b"], str)) and np.array_equal(box["b"], ref_b),
          a_resume_equal=np.array_equal(res_a, ref_a), done=done)
@@ -602,8 +630,9 @@ np.savez(sys.argv[2], a_cancelled=isinstance(box["a"], str) and "cancel" in box[
 def test_cancel_one_of_two_concurrent_renders(gpu, tmp_path):
     """The in-flight launches a cancel moves are those of the cancelled render only (cancel_pool_launches
     keys them by the scene's cancel word): two progressive renders of two scenes run at once on two
-    threads, one is cancelled mid-frame — the other finishes bit-identical to its own uninterrupted
-    render, and the cancelled one's checkpoint resumes bit-exactly."""
+    threads, one is cancelled mid-frame (rt_cancel from its 3rd progress call) — the other finishes
+    bit-identical to its own uninterrupted render, and the cancelled one's checkpoint resumes
+    bit-exactly."""
     import os
     import subprocess
     import sys
@@ -612,6 +641,7 @@ def test_cancel_one_of_two_concurrent_renders(gpu, tmp_path):
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]
     r = np.load(tmp_path / "t.npz")
+    print(p.stderr[-600:])
     print(f"cancelled render's checkpoint: {int(r['done'])} samples")
     assert bool(r["a_cancelled"])
     assert bool(r["b_equal"])
