@@ -1,6 +1,6 @@
 """Fused-batch stress (DEV TOOL): many progressive renders with random batch sizes, previews and random
-cancels; every finished render must equal the same render in one batch up to the pool's summation
-order (SUM_RTOL), every cancelled one must leave a checkpoint that resumes to the uninterrupted sums
+cancels (a quarter of them 1080p, where the pool's chunk rule matters); every finished render must equal
+the same render in one batch up to the pool's summation order (SUM_RTOL), every cancelled one must leave a checkpoint that resumes to the uninterrupted sums
 bit for bit.  A third of the renders deal their batches to devices=[0, 0] or [0, 0, 0] (the whole-batch
 split, one fused launch per device since round 5; bit-identical to one device).
 usage: python scripts/stress_fused.py [renders]"""
@@ -22,9 +22,11 @@ t0 = time.time()
 bad = 0
 for i in range(n):
     name = rnd.choice(list(scenes))
-    w, h = rnd.choice([(160, 90), (320, 180), (96, 64)])
-    spp = rnd.choice([8, 12, 24, 32])
-    batch = rnd.choice([1, 2, 3, 4, 5, 8])
+    w, h = rnd.choice([(160, 90), (320, 180), (96, 64), (1920, 1080)])
+    # 1080p: >= 64k pool items, where the chunk rule leaves its floor of 4 samples, so a resume's chunks
+    # differ unless they follow the whole render's rule (round 5's one-batch-left bug)
+    spp = rnd.choice([8, 12, 24, 32]) if w < 1920 else rnd.choice([24, 32, 48])
+    batch = rnd.choice([1, 2, 3, 4, 5, 8]) if w < 1920 else rnd.choice([8, 12, 16])
     rt = GpuRayTracer(w, h, seed=i)
     assert rt.load_from_json(scenes[name])
     rt.update_render_settings({"samples": spp, "maxBounces": 5})
