@@ -12,6 +12,7 @@ for spec in "$@"; do
   for src in $SRCS; do
     obj="$OUT/$name.${src%.*}.o"
     extra=""; [ $src = pt_onewave.hip ] && [ -z "$NO_TRK" ] && extra="-mllvm -amdgpu-use-amdgpu-trackers=1"
+    [ $src = pt_onewave.hip ] && extra="$extra $EXTRA_OW"   # (A/B: flags for the one-wave TU only)
     /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -mllvm -structurizecfg-skip-uniform-regions=1 $extra $flags -I "$ROOT/include" \
       -c "$ROOT/blenderraytracer_amd/csrc/$src" -o "$obj" &
     objs="$objs $obj"
