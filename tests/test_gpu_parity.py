@@ -524,21 +524,23 @@ from blenderraytracer_amd import capi
 from blenderraytracer_amd.renderer import GpuRayTracer
 from blenderraytracer_amd.scene import load_scene_json
 devices = json.loads(sys.argv[3])
+scene, spp = (sys.argv[4], int(sys.argv[5])) if len(sys.argv) > 5 else ("rtow.json", 512)
+batch = spp // 4
 def tracer():
     rt = GpuRayTracer(1920, 1080, seed=5)
-    assert rt.load_from_json(load_scene_json("rtow.json"))
-    rt.update_render_settings({"maxBounces": 5, "samples": 512})
+    assert rt.load_from_json(load_scene_json(scene))
+    rt.update_render_settings({"maxBounces": 5, "samples": spp})
     return rt
 rt = tracer()
-rt.render(batch_samples=128, devices=devices)                         # warm-up (scene, replicas, slots)
+rt.render(batch_samples=batch, devices=devices)                       # warm-up (scene, replicas, slots)
 t = time.perf_counter()
-full = rt.render(want=("mean",), batch_samples=128, devices=devices)
+full = rt.render(want=("mean",), batch_samples=batch, devices=devices)
 frame_s = time.perf_counter() - t
 lib = capi.load_library()
 box = {}
 def run():
     try:
-        rt.render(batch_samples=128, devices=devices)
+        rt.render(batch_samples=batch, devices=devices)
         box["rc"] = 0
     except RuntimeError as e:
         box["rc"] = str(e)
@@ -551,7 +553,7 @@ capi.check(lib.rt_cancel(rt.scene_handle()))
 th.join()
 sums, done = rt.checkpoint()
 rt2 = tracer()
-res = rt2.render(want=("mean",), resume=(sums, done), batch_samples=128, devices=devices)
+res = rt2.render(want=("mean",), resume=(sums, done), batch_samples=batch, devices=devices)
 np.savez(sys.argv[2], latency=box["t"] - t0, frame=frame_s, done=done, rc=str(box["rc"]),
          equal=np.array_equal(res["mean"], full["mean"]))
 '''
@@ -646,6 +648,29 @@ def test_cancel_one_of_two_concurrent_renders(gpu, tmp_path):
     assert bool(r["a_cancelled"])
     assert bool(r["b_equal"])
     assert bool(r["a_resume_equal"])
+
+
+def test_cancel_latency_triangle_scene(gpu, tmp_path):
+    """The same in-batch cancel on config 5 (mesh50k 1920x1080 x 256 spp in four batches): its walk runs
+    in the one-wave pool kernel, whose workgroups read the cancel word as their item starts (the LDS
+    kernels' queue move does not apply).  Measured 25 ms against a 114-ms frame: the items in flight
+    finish in ~1 ms, but the fused launch's remaining one-wave workgroups (~400k) still pass through the
+    dispatcher, each exiting after its read.  Asserted: rt_render returns within half a frame and the
+    checkpoint resumes bit-exactly."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", _CANCEL_SCRIPT, root, str(tmp_path / "c.npz"), "null", "mesh50k", "256"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    r = np.load(tmp_path / "c.npz")
+    latency, frame, done = float(r["latency"]), float(r["frame"]), int(r["done"])
+    print(f"cancel-to-return {latency * 1e3:.2f} ms; frame {frame * 1e3:.1f} ms; checkpoint {done} samples; {r['rc']}")
+    assert "CANCELLED" in str(r["rc"])
+    assert done in (0, 64, 128, 192)
+    assert latency < frame / 2
+    assert bool(r["equal"])
 
 
 def test_config4_rtow_4k_1024spp_sharded(gpu):
