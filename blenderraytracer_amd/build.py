@@ -92,11 +92,16 @@ def build_lib(force=False):
     deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(REPO, "include", f) for f in os.listdir(os.path.join(REPO, "include"))]
     if not force and not _stale(target, deps):
         return target
-    objs = []
-    for src in SOURCES:
+    objs, procs = [], []
+    for src in SOURCES:                  # the translation units compile in parallel
         obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
-        _run([HIPCC, *HIP_FLAGS, *SOURCE_FLAGS.get(src, []), "-c", os.path.join(CSRC, src), "-o", obj])
+        cmd = [HIPCC, *HIP_FLAGS, *SOURCE_FLAGS.get(src, []), "-c", os.path.join(CSRC, src), "-o", obj]
+        print(" ".join(cmd), flush=True)
+        procs.append((cmd, subprocess.Popen(cmd)))
         objs.append(obj)
+    failed = [cmd for cmd, p in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
     _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", target, *objs])
     write_build_info()
     return target

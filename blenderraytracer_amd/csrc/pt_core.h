@@ -255,6 +255,8 @@ struct SceneView {
     const Bvh2Node* sphere_wide;   // two-child nodes of the two trees (preorder)
     const Bvh2Node* tri_wide;
     int num_sphere_wide, num_tri_wide;
+    int tri_lds_nodes;             // ACC_BVH_TRI_LDS: the triangle tree's nodes [0, tri_lds_nodes) are read
+                                   // from the workgroup's LDS copy (set per launch, pt_trace.hip)
     int stack_entries;             // deepest leaf of the two trees (>= 1): the ordered walk's stack bound
     const SphereLeaf<R>* big_spheres;   // dominant spheres kept out of the sphere tree (scene_pack.h)
     int num_big_spheres;
@@ -692,9 +694,17 @@ typedef unsigned int rt_u4 __attribute__((ext_vector_type(4)));
 // gcell / grec: the grid's cell offsets and records copied to LDS (ACC_GRID_LDS): binary64 keeps the
 // 16-B binary32 filters there (the rest of a record is read from grid_leaf by filter survivors only),
 // binary32 the whole 32-B records (grec[2k], grec[2k + 1])
+// the triangle tree's breadth-first prefix (scene_pack.h make_wide): at most this many of its top nodes
+// are staged in LDS (ACC_BVH_TRI_LDS; 1023 = nine full levels and half the tenth)
+#ifndef RT_TRI_TOP_NODES
+#define RT_TRI_TOP_NODES 1023
+#endif
+// ntop (ACC_BVH_TRI_LDS): box / kid hold the triangle tree's first ntop nodes (its breadth-first top
+// levels, scene_pack.h make_wide); nodes from ntop on are read from global memory
 struct BvhStack {
     int* base; int stride; const rt_u4* box = nullptr; const rt_u2* kid = nullptr;
     const int* gcell = nullptr; const rt_u4* grec = nullptr;
+    int ntop = 0;
 };
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -765,7 +775,11 @@ RT_HD Bvh2Node load_node_lds(const BvhStack& s, int i) {
 // host cross-check).  Variants measured slower and removed: postponed leaves,
 // "while-while" leaf batching, binary16 child boxes, four-child nodes, stack top in a register, leaf
 // records as buffer loads.
-template <bool WIDE, bool LDSN = false, class Leaf>
+// LDSN: 0 every node from global memory; 1 every node from the LDS copy in stk (the sphere tree,
+// ACC_BVH_SPHERES_LDS); 2 nodes [0, stk.ntop) from the LDS copy, the others from global memory (the
+// triangle tree's top levels, ACC_BVH_TRI_LDS).  Wave-uniform steps read the node with scalar loads in
+// every mode.
+template <bool WIDE, int LDSN = 0, class Leaf>
 RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const BvhRay& br, const float& tl,
                     BvhStack stk, Work& w, Leaf&& leaf) {
     if constexpr (WIDE) {
@@ -812,10 +826,19 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
                 // every active lane at the same node (30 % of RTOW walk steps, 49 % on mesh50k): read
                 // it with scalar loads, which bypass the vector memory pipeline (+3.5 %)
                 const int first = __builtin_amdgcn_readfirstlane(cur);
-                if constexpr (LDSN) down = __ballot(cur != first) == 0 ? step(wide[first]) : step(load_node_lds(stk, cur));
-                else down = __ballot(cur != first) == 0 ? step(wide[first]) : step(load_node(wrs, cur));
+                if constexpr (LDSN == 1) down = __ballot(cur != first) == 0 ? step(wide[first]) : step(load_node_lds(stk, cur));
+                else if constexpr (LDSN == 2) {
+                    if (__ballot(cur != first) == 0) {
+                        down = step(wide[first]);
+                    } else {
+                        Bvh2Node n;                   // one slab test for both sources
+                        if (cur < stk.ntop) n = load_node_lds(stk, cur);
+                        else n = load_node(wrs, cur);
+                        down = step(n);
+                    }
+                } else down = __ballot(cur != first) == 0 ? step(wide[first]) : step(load_node(wrs, cur));
 #else
-                down = step(LDSN ? load_node_lds(stk, cur) : wide[cur]);
+                down = step(LDSN == 1 || (LDSN == 2 && cur < stk.ntop) ? load_node_lds(stk, cur) : wide[cur]);
 #endif
                 if (down) continue;
             } else {
@@ -948,7 +971,8 @@ RT_HD void tri_leaf_filtered(const SceneView<R>& sc, int fc, const TriRay& tr, V
 // stackless preorder walk.
 // TRI = false (ACC_BVH_SPHERES): scenes without triangles; the triangle walk's code is left out.
 // LDSN: the sphere tree's nodes are read from their LDS copy in stk (ACC_BVH_SPHERES_LDS).
-template <class R, bool WIDE, bool TRI = true, bool LDSN = false>
+// TLDS: the triangle tree's top levels are read from their LDS copy in stk (ACC_BVH_TRI_LDS).
+template <class R, bool WIDE, bool TRI = true, bool LDSN = false, bool TLDS = false>
 RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
     const R tmin = (R)0.001;
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
@@ -963,16 +987,16 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
         if (sc.num_big_spheres > 0) sphere_records(sc.big_spheres, 0, sc.num_big_spheres, o, d, a, fr, tmin, b, tl, w, true);
         auto leaf = [&](int fc) { sphere_leaf(sc, fc, o, d, a, fr, tmin, b, tl, w); };
         if (sc.num_sphere_nodes > 0)
-            bvh_walk<WIDE, LDSN>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w, leaf);
+            bvh_walk<WIDE, LDSN ? 1 : 0>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w, leaf);
     }
     if (TRI && sc.num_tri_nodes > 0) {
         if constexpr (sizeof(R) == 8 && RT_TRI_FILTER != 0) {
             const TriRay tr = make_tri_ray(o, d);
             auto leaf = [&](int fc) { tri_leaf_filtered(sc, fc, tr, o, d, tmin, b, tl, w); };
-            bvh_walk<WIDE>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, leaf);
+            bvh_walk<WIDE, TLDS ? 2 : 0>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, leaf);
         } else {
             auto leaf = [&](int fc) { tri_leaf(sc, fc, o, d, tmin, b, tl, w); };
-            bvh_walk<WIDE>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, leaf);
+            bvh_walk<WIDE, TLDS ? 2 : 0>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, leaf);
         }
     }
     return b;
@@ -1163,8 +1187,10 @@ RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work
 // ACC_BVH_SPHERES_LDS: the same walk with the sphere tree's nodes in LDS (trace_pool_lds_kernel)
 // ACC_GRID: sphere-only scenes through the uniform grid (closest_hit_grid)
 // ACC_GRID_LDS: the same walk with the grid's cell offsets and records (binary64: their filters) in LDS
+// ACC_BVH_TRI_LDS: the general ordered walk (scenes with triangles) with the triangle tree's top levels in
+// LDS (trace_pool_lds_kernel's persistent multi-wave workgroups, round 6)
 enum Accel : int { ACC_BRUTE = 0, ACC_BVH = 2, ACC_BVH_STACK = 3, ACC_BVH_SPHERES = 4, ACC_BVH_SPHERES_LDS = 5,
-                   ACC_GRID = 6, ACC_GRID_LDS = 7 };
+                   ACC_GRID = 6, ACC_GRID_LDS = 7, ACC_BVH_TRI_LDS = 8 };
 
 template <class R, int ACC>
 RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
@@ -1174,6 +1200,7 @@ RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
     else if constexpr (ACC == ACC_BVH_SPHERES_LDS) return closest_hit_bvh<R, true, false, true>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_GRID) return closest_hit_grid<R>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_GRID_LDS) return closest_hit_grid<R, true>(sc, o, d, w, stk);
+    else if constexpr (ACC == ACC_BVH_TRI_LDS) return closest_hit_bvh<R, true, true, false, true>(sc, o, d, w, stk);
     else return closest_hit<R>(sc, o, d);
 }
 

@@ -128,6 +128,7 @@ struct FinalizeParams {
 // device pow is not monotone (exceptions: tm and its byte), found by scanning +-kGammaScan ulps of every
 // threshold; overflow: more exceptions than kGammaExc (the table is then not used)
 constexpr int kGammaExc = 1024, kGammaScan = 4096;
+constexpr double kGammaMin = 0.25, kGammaMax = 4.0;   // gammas whose tables are used (preview_thresholds_ok)
 struct GammaTable {
     double t[255];
     uint32_t n_exc, overflow;

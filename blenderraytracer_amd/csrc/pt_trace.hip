@@ -12,14 +12,18 @@
 // all record loads are wave-uniform scalar loads.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "pt_launch.h"
 #include "pool_order.h"
+#include "queue_slots.h"
 
 namespace rt {
 
@@ -76,13 +80,16 @@ constexpr bool dyn_stack() { return sizeof(R) == 4 || (RT_F64_DYN_STACK != 0 && 
 #endif
 // walks with a per-lane LDS stack (the ordered BVH walks)
 template <int ACC>
-constexpr bool uses_stack() { return ACC == ACC_BVH_STACK || ACC == ACC_BVH_SPHERES || ACC == ACC_BVH_SPHERES_LDS; }
+constexpr bool uses_stack() {
+    return ACC == ACC_BVH_STACK || ACC == ACC_BVH_SPHERES || ACC == ACC_BVH_SPHERES_LDS || ACC == ACC_BVH_TRI_LDS;
+}
 
 template <class R, int ACC>
 constexpr int waves_per_simd() {
     if constexpr (ACC == ACC_GRID || ACC == ACC_GRID_LDS) return sizeof(R) == 8 ? RT_GRID_WAVES_PER_SIMD : RT_GRID_WAVES_F32;
     if constexpr (ACC == ACC_BVH_SPHERES) return sizeof(R) == 8 ? RT_SPHERES_WAVES_PER_SIMD : RT_SPHERES_WAVES_F32;
     if constexpr (ACC == ACC_BVH_SPHERES_LDS) return sizeof(R) == 8 ? RT_LDS_OCC_F64 : RT_LDS_OCC_F32;
+    if constexpr (ACC == ACC_BVH_TRI_LDS) return sizeof(R) == 8 ? RT_BVH_WAVES_PER_SIMD : RT_BVH_WAVES_F32;
     return ACC >= ACC_BVH ? (sizeof(R) == 8 ? RT_BVH_WAVES_PER_SIMD : RT_BVH_WAVES_F32) : RT_MIN_WAVES_PER_SIMD;
 }
 
@@ -526,7 +533,8 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
 // workgroup's waves finish together and the copy is paid once per workgroup, not per item.  The items
 // are the one-wave kernel's (item = chunk * tiles + tile, same partials layout), and each is traced
 // exactly as there, so the sums are bit-identical to it.  The queue is one of kPoolQueues counter
-// pairs {next item, waves exited} (a ring, one per launch): the last wave to exit sets both back to 0.
+// pairs {next item, waves exited}, held by one launch at a time (acquire_queue / hold_queue, queue_slots.h):
+// the last wave to exit sets both back to 0.
 // Waves per workgroup: a multiple of 4, so that every workgroup puts the same number of waves on
 // each SIMD (10-wave workgroups at 5 waves/SIMD left one SIMD a wave short of the second workgroup:
 // one workgroup per CU, RTOW -28 %)
@@ -543,19 +551,28 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
 #ifndef RT_GRID_LDS_WAVES_F32
 #define RT_GRID_LDS_WAVES_F32 12  // 2 workgroups per CU at 6 waves/SIMD (8: 3 per CU, -0.7 %)
 #endif
+// the triangle tree's LDS kernel (ACC_BVH_TRI_LDS): one workgroup per CU at 4 waves/SIMD, so that the
+// CU's one copy of the top levels is as large as its LDS allows beside the 16 waves' stacks and partials
+// (binary32, 5 waves/SIMD: 4-wave workgroups, five copies per CU)
+#ifndef RT_TRI_LDS_WAVES_F64
+#define RT_TRI_LDS_WAVES_F64 16
+#endif
+#ifndef RT_TRI_LDS_WAVES_F32
+#define RT_TRI_LDS_WAVES_F32 4
+#endif
 template <class R, int ACC = ACC_BVH_SPHERES_LDS>
 constexpr int lds_waves() {
     if constexpr (ACC == ACC_GRID_LDS) return sizeof(R) == 8 ? RT_GRID_LDS_WAVES_F64 : RT_GRID_LDS_WAVES_F32;
+    if constexpr (ACC == ACC_BVH_TRI_LDS) return sizeof(R) == 8 ? RT_TRI_LDS_WAVES_F64 : RT_TRI_LDS_WAVES_F32;
     return sizeof(R) == 8 ? RT_LDS_WAVES_F64 : RT_LDS_WAVES_F32;
 }
 constexpr int kPoolQueues = 1024;
 __device__ uint32_t g_pool_queue[2 * kPoolQueues];
 
-// the sphere tree's two-child nodes into LDS: child boxes at box[3k .. 3k+2], references at kid[k]
-template <class R>
-__device__ __forceinline__ void copy_nodes_lds(const SceneView<R>& sc, rt_u4* box, rt_u2* kid, int t, int threads) {
-    for (int k = t; k < sc.num_sphere_wide; k += threads) {
-        const rt_u4* g = reinterpret_cast<const rt_u4*>(sc.sphere_wide + k);
+// two-child nodes [0, n) into LDS: child boxes at box[3k .. 3k+2], references at kid[k]
+__device__ __forceinline__ void copy_wide_lds(const Bvh2Node* src, int n, rt_u4* box, rt_u2* kid, int t, int threads) {
+    for (int k = t; k < n; k += threads) {
+        const rt_u4* g = reinterpret_cast<const rt_u4*>(src + k);
         const rt_u4 q3 = g[3];
         box[3 * k] = g[0];
         box[3 * k + 1] = g[1];
@@ -585,12 +602,23 @@ void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, c
         copy_grid_lds(sc, grec, gcell, threadIdx.x, 64 * W);
         stk.gcell = gcell;
         stk.grec = grec;
+    } else if constexpr (ACC == ACC_BVH_TRI_LDS) {
+        // the triangle tree's breadth-first top levels (nodes [0, tri_lds_nodes)): the divergent node
+        // reads of a walk's first levels become ds_read_b128s (deeper nodes, leaves and the sphere tree
+        // stay in global memory)
+        const int n = sc.tri_lds_nodes, entries = min(sc.stack_entries, RT_BVH_STACK);
+        rt_u4* box = reinterpret_cast<rt_u4*>(lds_dyn);
+        rt_u2* kid = reinterpret_cast<rt_u2*>(lds_dyn + 48 * n);
+        int* stacks = reinterpret_cast<int*>(lds_dyn + 56 * n);
+        copy_wide_lds(sc.tri_wide, n, box, kid, threadIdx.x, 64 * W);
+        stk = BvhStack{stacks + wave * entries * 64 + lane, 64, box, kid};
+        stk.ntop = n;
     } else {
         const int n = sc.num_sphere_wide, entries = min(sc.stack_entries, RT_BVH_STACK);
         rt_u4* box = reinterpret_cast<rt_u4*>(lds_dyn);
         rt_u2* kid = reinterpret_cast<rt_u2*>(lds_dyn + 48 * n);
         int* stacks = reinterpret_cast<int*>(lds_dyn + 56 * n);
-        copy_nodes_lds(sc, box, kid, threadIdx.x, 64 * W);
+        copy_wide_lds(sc.sphere_wide, n, box, kid, threadIdx.x, 64 * W);
         stk = BvhStack{stacks + wave * entries * 64 + lane, 64, box, kid};
     }
     double* acc = acc_all + wave * 3 * 64;
@@ -626,6 +654,18 @@ void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, c
         }
     }
 }
+
+// RT_CAM_RELOAD (pt_path.h start_sample) reads the camera words at offsetof(SceneView, cam_o) of the
+// kernel-argument segment: that holds only while the LDS pool kernel's first parameter is TraceArgs<R>
+// by value (whose first member is the SceneView, static_assert above).  A signature change fails here
+// instead of reading the camera from the wrong bytes.
+template <class F> struct FirstParam;
+template <class A0, class... As> struct FirstParam<void (*)(A0, As...)> { using type = A0; };
+static_assert(std::is_same<FirstParam<decltype(&trace_pool_lds_kernel<float, false, ACC_GRID_LDS>)>::type,
+                           TraceArgs<float>>::value &&
+              std::is_same<FirstParam<decltype(&trace_pool_lds_kernel<float, true, ACC_BVH_SPHERES_LDS>)>::type,
+                           TraceArgs<float>>::value,
+              "the camera reload needs TraceArgs as the LDS pool kernel's first (by-value) argument");
 
 // sum[q] += part[c][tile][.][m] for c = 0 .. chunks-1 in chunk order (binary64); one thread per pixel,
 // one one-wave workgroup per tile (its reads of one chunk are 3 x 512 contiguous bytes).  One-wave
@@ -811,9 +851,107 @@ static size_t lds_nodes_bytes(const SceneView<R>& sc) {
     return b + (size_t)W * 3 * 64 * 8 + 256 <= budget ? b : 0;
 }
 
-// the next queue of the ring: one counter for every instantiation and thread, so launches in flight
-// together (streams, scenes, precisions) never share a queue
-static std::atomic<unsigned> g_next_queue{0};
+// Which launches of scenes with a triangle tree run trace_pool_lds_kernel<.., ACC_BVH_TRI_LDS> (the top
+// levels of the triangle tree in LDS): RT_LDS_TRI = 0 never, 1 (default) binary64, 2 both precisions.
+#ifndef RT_LDS_TRI
+#define RT_LDS_TRI 1
+#endif
+// the triangle-tree nodes a launch stages (0: the one-wave kernel): as many of the breadth-first prefix
+// (RT_TRI_TOP_NODES, or RT_TRI_LDS_NODES from the environment for A/B runs) as fit the CU's LDS beside
+// the workgroups' stacks and partials, at least 64
+template <class R>
+static int lds_tri_nodes(const SceneView<R>& sc) {
+    static const int v = [] {
+        const char* e = getenv("RT_LDS_TRI");
+        return e ? atoi(e) : RT_LDS_TRI;
+    }();
+    static const int cap = [] {
+        const char* e = getenv("RT_TRI_LDS_NODES");
+        return e ? std::max(0, std::min(atoi(e), RT_TRI_TOP_NODES)) : RT_TRI_TOP_NODES;
+    }();
+    if (v < (sizeof(R) == 8 ? 1 : 2) || sc.num_tri_wide <= 0) return 0;
+    constexpr int W = lds_waves<R, ACC_BVH_TRI_LDS>();
+    const long long budget = 160 * 1024 / (4 * waves_per_simd<R, ACC_BVH_TRI_LDS>() / W);
+    const long long fixed = (long long)W * std::min(sc.stack_entries, RT_BVH_STACK) * 64 * 4 + (long long)W * 3 * 64 * 8 + 256;
+    const long long n = std::min<long long>({(long long)sc.num_tri_wide, (long long)cap, (budget - fixed) / 56});
+    return n >= 64 ? (int)n : 0;
+}
+template <class R>
+static size_t lds_tri_bytes(const SceneView<R>& sc, int nodes) {
+    return (size_t)56 * nodes + (size_t)lds_waves<R, ACC_BVH_TRI_LDS>() * std::min(sc.stack_entries, RT_BVH_STACK) * 64 * 4;
+}
+
+// ---- ownership of the LDS pool launches' queues (queue_slots.h) ----
+// Per device, kPoolQueues counter pairs (g_pool_queue, device memory); a launch holds its pair from
+// acquire_queue() until the pair's event — recorded on the launch's stream after the launch
+// (hold_queue), and again after a cancel's clear kernel — has completed.  Launches in flight together
+// (streams, scenes, precisions, threads) therefore never share a pair.  Every call is under
+// g_launch_mu, which also makes cancel_pool_launches' check (the launch still holds its pair) and act
+// (the move, the clear, the later release) one step.
+namespace {
+std::mutex g_launch_mu;
+QueueSlots<hipEvent_t>* g_slots[64];      // per device, created on first use (under g_launch_mu)
+
+QueueSlots<hipEvent_t>& device_slots(int dev) {
+    QueueSlots<hipEvent_t>*& s = g_slots[dev & 63];
+    if (!s) s = new QueueSlots<hipEvent_t>(kPoolQueues);   // lives as long as the process
+    return *s;
+}
+// a slot's release event has completed (never recorded: complete; a device error: nothing will
+// complete later either, the launch that failed reports it)
+bool release_done(hipEvent_t ev) {
+    if (!ev) return true;
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipErrorNotReady) return false;
+    if (q != hipSuccess) (void)hipGetLastError();
+    return true;
+}
+}  // namespace
+
+// a queue pair of the current device for one LDS launch: waits (20-us sleeps) while every pair is held,
+// which takes kPoolQueues launches in flight on one device
+static hipError_t acquire_queue(int* dev, int* qi) {
+    hipError_t e = hipGetDevice(dev);
+    if (e != hipSuccess) return e;
+    for (;;) {
+        {
+            std::lock_guard<std::mutex> g(g_launch_mu);
+            QueueSlots<hipEvent_t>& s = device_slots(*dev);
+            const int k = s.acquire(release_done);
+            if (k >= 0) {
+                if (!s.token(k)) e = hipEventCreateWithFlags(&s.token(k), hipEventDisableTiming);
+                if (e != hipSuccess) {
+                    s.token(k) = nullptr;
+                    s.abandon(k);
+                    return e;
+                }
+                *qi = k;
+                return hipSuccess;
+            }
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+// after the launch on `stream` (launched: false when it failed to enqueue): the pair is held until the
+// launch has ended
+static hipError_t hold_queue(int dev, int qi, hipStream_t stream, bool launched) {
+    std::lock_guard<std::mutex> g(g_launch_mu);
+    QueueSlots<hipEvent_t>& s = device_slots(dev);
+    if (!launched) {
+        s.abandon(qi);
+        return hipSuccess;
+    }
+    const hipError_t e = hipEventRecord(s.token(qi), stream);
+    if (e != hipSuccess) {
+        // not recorded: the event's last record (complete, or never recorded) would free the pair
+        // while the launch may run, so the pair is waited for here instead
+        (void)hipStreamSynchronize(stream);
+        s.abandon(qi);
+        return e;
+    }
+    s.hold(qi, s.token(qi));
+    return hipSuccess;
+}
 
 // ---- cancelling LDS pool launches in flight (pt_launch.h: cancel_pool_launches) ----
 // The queue of launch qi moved to `items`: takes from then on return >= items.  aborted is stored first
@@ -825,7 +963,7 @@ __global__ __launch_bounds__(64) void queue_cancel_kernel(const int qi, const ui
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope
     __hip_atomic_fetch_max(g_pool_queue + 2 * qi, items, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// after the launch (and the move) ended: the queue pair back to 0 for the ring's next user
+// after the launch (and the move) ended: the queue pair back to 0 for its next holder
 __global__ __launch_bounds__(64) void queue_clear_kernel(const int qi) {
     if (threadIdx.x < 2) __hip_atomic_store(g_pool_queue + 2 * qi + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -835,43 +973,36 @@ struct PoolLaunch {
     const uint32_t* cancel;
     uint32_t* aborted;
     int device, qi;
+    unsigned gen;                         // the pair's generation (QueueSlots::generation) for this launch
     uint32_t items;
     hipStream_t stream;
-    hipEvent_t done;                      // recorded after the launch
 };
-std::mutex g_launch_mu;
 std::vector<PoolLaunch> g_launches;       // launches that may still run (pruned as they are found done)
 hipStream_t g_cancel_stream[64];          // per device, created on first use (under g_launch_mu)
 
-// drop the records for which keep() is false (their events destroyed)
+// drop the records for which keep() is false
 template <class F>
 void prune_launches(F keep) {
     size_t w = 0;
-    for (size_t k = 0; k < g_launches.size(); ++k) {
+    for (size_t k = 0; k < g_launches.size(); ++k)
         if (keep(g_launches[k])) g_launches[w++] = g_launches[k];
-        else if (g_launches[k].done) (void)hipEventDestroy(g_launches[k].done);
-    }
     g_launches.resize(w);
 }
-bool launch_done(const PoolLaunch& l) { return !l.done || hipEventQuery(l.done) == hipSuccess; }
+// the launch has ended: its pair's release event completed (then the pair may have been handed to
+// another launch since, which the generation shows).  Under g_launch_mu.
+bool launch_done(const PoolLaunch& l) {
+    QueueSlots<hipEvent_t>& s = device_slots(l.device);
+    return s.generation(l.qi) != l.gen || !s.held(l.qi) || release_done(s.token(l.qi));
+}
 }  // namespace
 
-// after the launch was enqueued on `stream` (of the current device).  Records whose launch has ended
-// are dropped here and in cancel_pool_launches: a record is only ever acted on while its launch may
-// still hold its queue slot, never after the ring has handed that slot to another launch
-static hipError_t register_pool_launch(const Counters& c, int qi, uint32_t items, hipStream_t stream) {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    hipEvent_t ev = nullptr;
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventRecord(ev, stream);
-    if (e != hipSuccess) {
-        if (ev) (void)hipEventDestroy(ev);
-        return e;
-    }
+// after the launch was enqueued (and its pair held, hold_queue) on `stream` of device `dev`.  Records
+// whose launch has ended are dropped here and in cancel_pool_launches: a record is only acted on while
+// its launch still holds its pair (checked under the lock that hands pairs out)
+static hipError_t register_pool_launch(const Counters& c, int dev, int qi, uint32_t items, hipStream_t stream) {
     std::lock_guard<std::mutex> g(g_launch_mu);
     prune_launches([](const PoolLaunch& l) { return !launch_done(l); });
-    g_launches.push_back(PoolLaunch{c.cancel, c.aborted, dev, qi, items, stream, ev});
+    g_launches.push_back(PoolLaunch{c.cancel, c.aborted, dev, qi, device_slots(dev).generation(qi), items, stream});
     return hipSuccess;
 }
 
@@ -903,6 +1034,12 @@ hipError_t cancel_pool_launches(const uint32_t* cancel) {
             hipLaunchKernelGGL(queue_clear_kernel, dim3(1), dim3(64), 0, l.stream, l.qi);
             e = hipGetLastError();
         }
+        // the pair stays held until the clear has run (it waits for the move): no other launch can take
+        // it while the move may still land on it
+        QueueSlots<hipEvent_t>& slots = device_slots(l.device);
+        if (e == hipSuccess) e = hipEventRecord(slots.token(l.qi), l.stream);
+        if (e == hipSuccess) slots.extend(l.qi, slots.token(l.qi));
+        else (void)hipStreamSynchronize(l.stream);   // not recorded: the pair is released only once idle
         if (ev) (void)hipEventDestroy(ev);
         if (e != hipSuccess && err == hipSuccess) err = e;
         return false;                     // cancelled: the record goes
@@ -929,13 +1066,21 @@ static int device_cus() {
 }
 
 template <class R, int ACC>
-static hipError_t launch_pool_kernel(const TraceArgs<R>& a, bool count, double* part, int tiles, int chunks,
+static hipError_t launch_pool_kernel(const TraceArgs<R>& a0, bool count, double* part, int tiles, int chunks,
                                      int chunk, hipStream_t stream) {
-    if constexpr (ACC == ACC_BVH_SPHERES || ACC == ACC_GRID) {
-        constexpr int LACC = ACC == ACC_GRID ? ACC_GRID_LDS : ACC_BVH_SPHERES_LDS;
-        const size_t lb = ACC == ACC_GRID ? lds_grid_bytes(a.sc) : lds_nodes_bytes(a.sc);
+    if constexpr (ACC == ACC_BVH_SPHERES || ACC == ACC_GRID || ACC == ACC_BVH_STACK) {
+        constexpr int LACC = ACC == ACC_GRID ? ACC_GRID_LDS : ACC == ACC_BVH_STACK ? ACC_BVH_TRI_LDS : ACC_BVH_SPHERES_LDS;
+        TraceArgs<R> a = a0;
+        size_t lb = 0;
+        if constexpr (ACC == ACC_BVH_STACK) {
+            a.sc.tri_lds_nodes = lds_tri_nodes(a.sc);
+            lb = a.sc.tri_lds_nodes ? lds_tri_bytes(a.sc, a.sc.tri_lds_nodes) : 0;
+        } else {
+            lb = ACC == ACC_GRID ? lds_grid_bytes(a.sc) : lds_nodes_bytes(a.sc);
+        }
         if (lb) {
-            const int qi = (int)(g_next_queue++ % kPoolQueues);
+            int dev = 0, qi = 0;
+            if (const hipError_t e = acquire_queue(&dev, &qi)) return e;
             const long long items = (long long)tiles * chunks;
             constexpr int W = lds_waves<R, LACC>();
             const int resident = device_cus() * 4 * waves_per_simd<R, LACC>() / W;
@@ -945,11 +1090,14 @@ static hipError_t launch_pool_kernel(const TraceArgs<R>& a, bool count, double* 
             else hipLaunchKernelGGL((trace_pool_lds_kernel<R, false, LACC>), dim3(grid), dim3(64 * W), lb, stream,
                                     a, part, tiles, chunk, (int)items, qi);
             const hipError_t e = hipGetLastError();
-            if (e != hipSuccess || !a.c.cancel) return e;
-            return register_pool_launch(a.c, qi, (uint32_t)items, stream);
+            const hipError_t eh = hold_queue(dev, qi, stream, e == hipSuccess);
+            if (e != hipSuccess) return e;
+            if (eh != hipSuccess) return eh;
+            if (!a.c.cancel) return hipSuccess;
+            return register_pool_launch(a.c, dev, qi, (uint32_t)items, stream);
         }
     }
-    return launch_onewave_pool<R, ACC>(a, count, part, tiles, chunks, chunk, stream);
+    return launch_onewave_pool<R, ACC>(a0, count, part, tiles, chunks, chunk, stream);
 }
 
 template <class R, int ACC>
@@ -1145,7 +1293,7 @@ __global__ __launch_bounds__(64) void closest_hits_lds_kernel(const SceneView<R>
     const int nn = sc.num_sphere_wide;
     rt_u4* box = reinterpret_cast<rt_u4*>(lds_dyn);
     rt_u2* kid = reinterpret_cast<rt_u2*>(lds_dyn + 48 * nn);
-    copy_nodes_lds(sc, box, kid, threadIdx.x, 64);
+    copy_wide_lds(sc.sphere_wide, nn, box, kid, threadIdx.x, 64);
     __syncthreads();
     const BvhStack stk{reinterpret_cast<int*>(lds_dyn + 56 * nn) + threadIdx.x, 64, box, kid};
     const size_t r = (size_t)blockIdx.x * 64 + threadIdx.x;
@@ -1183,13 +1331,43 @@ __global__ __launch_bounds__(64) void closest_hits_grid_lds_kernel(const SceneVi
     idx_out[r] = c.kind == HIT_NONE ? -1 : c.idx;
 }
 
+// ... through the LDS copy of the triangle tree's top levels (trace_pool_lds_kernel<.., ACC_BVH_TRI_LDS>'s
+// walk; sc.tri_lds_nodes set by the launch)
+template <class R>
+__global__ __launch_bounds__(64) void closest_hits_tri_lds_kernel(const SceneView<R> sc, const double* __restrict__ rays,
+                                                                  const size_t n, double* __restrict__ t_out,
+                                                                  int* __restrict__ kind_out, int* __restrict__ idx_out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_dyn[];   // [boxes][references][stack]
+    const int nn = sc.tri_lds_nodes;
+    rt_u4* box = reinterpret_cast<rt_u4*>(lds_dyn);
+    rt_u2* kid = reinterpret_cast<rt_u2*>(lds_dyn + 48 * nn);
+    copy_wide_lds(sc.tri_wide, nn, box, kid, threadIdx.x, 64);
+    __syncthreads();
+    BvhStack stk{reinterpret_cast<int*>(lds_dyn + 56 * nn) + threadIdx.x, 64, box, kid};
+    stk.ntop = nn;
+    const size_t r = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (r >= n) return;
+    const double* q = rays + 6 * r;
+    const V3<R> o = mk<R>((R)q[0], (R)q[1], (R)q[2]), d = mk<R>((R)q[3], (R)q[4], (R)q[5]);
+    Work w{0, 0, 0, 0, 0, 0};
+    const Closest<R> c = closest_hit_acc<R, ACC_BVH_TRI_LDS>(sc, o, d, w, stk);
+    t_out[r] = c.kind == HIT_NONE ? (double)INFINITY : (double)c.t;
+    kind_out[r] = c.kind;
+    idx_out[r] = c.kind == HIT_NONE ? -1 : c.idx;
+}
+
 template <class R>
 hipError_t launch_closest_hits(const SceneView<R>& sc, bool bvh, const double* rays, size_t n, double* t, int* kind,
                                int* idx, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 63) / 64));
     const bool spheres = bvh && bvh_walk_mode(sc) == ACC_BVH_SPHERES;   // the walk the trace kernel runs
-    if (spheres && lds_nodes_bytes(sc)) {
+    if (bvh && bvh_walk_mode(sc) == ACC_BVH_STACK && lds_tri_nodes(sc)) {
+        SceneView<R> v = sc;
+        v.tri_lds_nodes = lds_tri_nodes(sc);
+        const size_t lb = (size_t)56 * v.tri_lds_nodes + (size_t)std::min(sc.stack_entries, RT_BVH_STACK) * 64 * 4;
+        hipLaunchKernelGGL((closest_hits_tri_lds_kernel<R>), grid, dim3(64), lb, stream, v, rays, n, t, kind, idx);
+    } else if (spheres && lds_nodes_bytes(sc)) {
         const size_t lb = (size_t)56 * sc.num_sphere_wide + (size_t)std::min(sc.stack_entries, RT_BVH_STACK) * 64 * 4;
         hipLaunchKernelGGL((closest_hits_lds_kernel<R>), grid, dim3(64), lb, stream, sc, rays, n, t, kind, idx);
     } else if (spheres)
@@ -1334,11 +1512,15 @@ __global__ __launch_bounds__(64) void preview_kernel(const FinalizeParams p, con
     *reinterpret_cast<uint32_t*>(rgba8 + 4 * q) = o;
 }
 
-// thresholds of gamma_byte for this gamma; false when 1/gamma is not a finite positive number (the byte is
-// then not a non-decreasing function of tm, and previews take finalize_kernel)
+// thresholds of gamma_byte for this gamma: only for gammas in [kGammaMin, kGammaMax] (pt_launch.h), the
+// range where the +-kGammaScan-ulp exception scan is verified to find every value at which the device
+// pow is not monotone (tests/test_gpu_parity.py::test_preview_thresholds_match_finalize checks
+// +-3000 ulps around every threshold at both ends and inside).  The width of such a region grows with
+// gamma, so outside the range — and when 1/gamma is not a finite positive number, where the byte is not a
+// non-decreasing function of tm at all — RGBA8-only epilogues and previews take finalize_kernel.
 bool preview_thresholds_ok(double gamma) {
     const double ig = 1.0 / gamma;
-    return ig > 0.0 && ig < INFINITY;
+    return ig > 0.0 && ig < INFINITY && gamma >= kGammaMin && gamma <= kGammaMax;
 }
 hipError_t launch_gamma_thresholds(double gamma, GammaTable* T, hipStream_t stream) {
     hipLaunchKernelGGL(gamma_thresholds_kernel, dim3(1), dim3(256), 0, stream, 1.0 / gamma, T);

@@ -269,6 +269,44 @@ struct DescCopy {
 
 }  // namespace
 
+// The RGBA8 threshold table of one gamma (launch_gamma_thresholds) on the scene's device.  A table is
+// built once and then only read: an asynchronous epilogue on any stream reads its own gamma's table, so
+// a later call with another gamma can never overwrite the bytes an earlier one is still reading (ADVICE
+// r5).  `used` is recorded after every kernel that reads the table; a slot is rebuilt for another gamma
+// (the least recently used one, when kGammaSlots gammas are in use) only after it has completed.
+struct GammaSlot {
+    DevBuf<unsigned char> buf;
+    double gamma = NAN;
+    bool ok = false;                 // no exception overflow: the table may be used
+    hipEvent_t used = nullptr;
+    bool used_recorded = false;
+    uint64_t tick = 0;               // last use (LRU)
+    const GammaTable* table() const { return reinterpret_cast<const GammaTable*>(buf.p); }
+    void release() {
+        buf.release();
+        if (used) (void)hipEventDestroy(used);
+        used = nullptr;
+    }
+};
+constexpr int kGammaSlots = 8;
+
+// What a resident checkpoint's sums are sums of: a resume from the sums left on the device
+// (rt_render_resume with sums NULL) must name the same frame, crop window, first sample, precision, seed,
+// anti-aliasing mode and depth, not only the same pixel count.
+struct CkptKey {
+    int32_t width, height, x0, y0, cw, ch, sample_begin, precision, aa_mode, max_depth;
+    uint64_t seed;
+    bool operator==(const CkptKey& o) const {
+        return width == o.width && height == o.height && x0 == o.x0 && y0 == o.y0 && cw == o.cw && ch == o.ch &&
+               sample_begin == o.sample_begin && precision == o.precision && aa_mode == o.aa_mode &&
+               max_depth == o.max_depth && seed == o.seed;
+    }
+};
+inline CkptKey ckpt_key(const rt_settings* s, int cw, int ch) {
+    return CkptKey{s->width, s->height, s->crop_x0, s->crop_y0, cw, ch, std::max(0, s->sample_begin), s->precision,
+                   s->aa_mode, s->max_depth, (uint64_t)s->seed};
+}
+
 // A shard's staging buffers on the home device and the events that free them (merge_shards,
 // trace_replica).
 struct MergeSlot {
@@ -311,16 +349,16 @@ struct rt_scene {
     std::vector<uint8_t*> preview_dev;    // the same buffers' device addresses
     size_t preview_host_n = 0;
     std::vector<hipEvent_t> batch_done;   // home stream: batch k's reduce, merges and preview done (slot k % ring)
-    // preview frames / RGBA8-only epilogues: the gamma table of gamma gamma_t_of (launch_gamma_thresholds)
-    // and whether it can be used (no exception overflow)
-    DevBuf<unsigned char> gamma_t;
-    double gamma_t_of = NAN;
-    bool gamma_t_ok = false;
+    // preview frames / RGBA8-only epilogues: the gamma tables (launch_gamma_thresholds), one per gamma,
+    // never rebuilt while a kernel may read them (gamma_table)
+    std::vector<GammaSlot> gamma_slots;
+    uint64_t gamma_tick = 0;
     std::atomic<int> cancel{0};
     uint32_t* ctl = nullptr;        // the render's control words (kCtl*), host address
     uint32_t* ctl_dev = nullptr;    // ... their device address (portable mapping: valid on every device)
     size_t ckpt_pixels = 0;         // progressive state of the last rt_render / rt_render_resume:
     int ckpt_done = 0;              // `home.sum` holds samples [sample_begin, ckpt_done) of ckpt_pixels pixels
+    CkptKey ckpt_key{};             // ... of this frame, crop, first sample, precision and seed
 };
 
 namespace {
@@ -351,26 +389,52 @@ int check_settings(const rt_settings* s, int* cw, int* ch) {
     return RT_OK;
 }
 
-// The gamma table of `gamma` on the scene's device (built once per gamma on `st`, which is waited for, and
-// its exception count read back), or nullptr when previews must take finalize_kernel
-const GammaTable* gamma_table(rt_scene* sc, double gamma, hipStream_t st) {
+// The gamma table of `gamma` on the scene's device (current), or nullptr when previews must take
+// finalize_kernel.  A new gamma's table is built on the scene's own stream (`home.stream`, waited for:
+// its exception count is read back) into a slot no kernel is reading: a free one, else the least
+// recently used slot once its last reader has completed.  The caller's stream is never synchronized.
+GammaSlot* gamma_table(rt_scene* sc, double gamma) {
     if (!preview_thresholds_ok(gamma)) return nullptr;
-    if (!(sc->gamma_t_of == gamma)) {
+    GammaSlot* g = nullptr;
+    for (GammaSlot& x : sc->gamma_slots)
+        if (x.gamma == gamma) g = &x;
+    if (!g) {
+        sc->gamma_slots.reserve(kGammaSlots);      // never reallocated: a render keeps its slot's address
+        if ((int)sc->gamma_slots.size() < kGammaSlots) {
+            sc->gamma_slots.emplace_back();
+            g = &sc->gamma_slots.back();
+        } else {
+            g = &sc->gamma_slots[0];
+            for (GammaSlot& x : sc->gamma_slots)
+                if (x.tick < g->tick) g = &x;
+        }
+        hipError_t e = g->used_recorded ? hipEventSynchronize(g->used) : hipSuccess;
+        g->gamma = NAN;
+        g->used_recorded = false;
         uint32_t words[2] = {0, 1};
-        hipError_t e = sc->gamma_t.ensure(sizeof(GammaTable));
-        GammaTable* g = reinterpret_cast<GammaTable*>(sc->gamma_t.p);
-        if (e == hipSuccess) e = launch_gamma_thresholds(gamma, g, st);
-        if (e == hipSuccess) e = hipMemcpyAsync(words, &g->n_exc, sizeof words, hipMemcpyDeviceToHost, st);
+        hipStream_t st = sc->home.stream;
+        if (e == hipSuccess && !g->used) e = hipEventCreateWithFlags(&g->used, hipEventDisableTiming);
+        if (e == hipSuccess) e = g->buf.ensure(sizeof(GammaTable));
+        GammaTable* t = reinterpret_cast<GammaTable*>(g->buf.p);
+        if (e == hipSuccess) e = launch_gamma_thresholds(gamma, t, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(words, &t->n_exc, sizeof words, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) {
             (void)hipGetLastError();
-            sc->gamma_t_of = NAN;
             return nullptr;
         }
-        sc->gamma_t_of = gamma;
-        sc->gamma_t_ok = words[1] == 0;
+        g->gamma = gamma;
+        g->ok = words[1] == 0;
     }
-    return sc->gamma_t_ok ? reinterpret_cast<const GammaTable*>(sc->gamma_t.p) : nullptr;
+    g->tick = ++sc->gamma_tick;
+    return g->ok ? g : nullptr;
+}
+
+// after a kernel reading g's table was enqueued on `st`
+hipError_t gamma_used(GammaSlot* g, hipStream_t st) {
+    const hipError_t e = hipEventRecord(g->used, st);
+    if (e == hipSuccess) g->used_recorded = true;
+    return e;
 }
 
 // mean, toneMap, gammaCorrect (+ PostProcessor.denoise), RGBA8 on `st` (ray-tracer.js:208-276).
@@ -380,7 +444,10 @@ hipError_t epilogue(rt_scene* sc, const rt_settings* s, int cw, int ch, const do
                     uint8_t* rgba, hipStream_t st, bool thresholds = false) {
     FinalizeParams fp{cw * ch, s->samples, s->tone_map, s->exposure, s->gamma};
     if (thresholds && !s->denoise && !mean && !post && rgba)
-        if (const GammaTable* g = gamma_table(sc, s->gamma, st)) return launch_finalize(fp, sum, nullptr, nullptr, rgba, st, g);
+        if (GammaSlot* g = gamma_table(sc, s->gamma)) {
+            const hipError_t e = launch_finalize(fp, sum, nullptr, nullptr, rgba, st, g->table());
+            return e == hipSuccess ? gamma_used(g, st) : e;
+        }
     if (!s->denoise) return launch_finalize(fp, sum, mean, post, rgba, st);
     hipError_t e = sc->post_raw.ensure(4 * (size_t)cw * ch);
     if (e == hipSuccess) e = launch_finalize(fp, sum, mean, sc->post_raw.p, nullptr, st);
@@ -786,7 +853,7 @@ void rt_scene_destroy(rt_scene* sc) {
     sc->mean.release(); sc->post.release(); sc->post_raw.release();
     for (MergeSlot& m : sc->merge) m.release();
     sc->rgba.release();
-    sc->gamma_t.release();
+    for (GammaSlot& g : sc->gamma_slots) g.release();
     for (uint8_t* p : sc->preview_host)
         if (p) (void)hipHostFree(p);
     if (sc->ctl) (void)hipHostFree(sc->ctl);
@@ -881,6 +948,9 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
     if (rc) return rc;
     std::vector<DeviceState*> states;
     if ((rc = shard_states(sc, s, states))) return rc;
+    // no checkpoint from here until the new sums are consistent (set below, with the samples they hold):
+    // a render that fails in between leaves none, rather than old metadata over overwritten sums
+    sc->ckpt_pixels = 0;
     sc->cancel.store(0);
     ctl_cancel(sc->ctl, 0);
     // this render's LDS pool launches are registered under its cancel word until it returns
@@ -1067,13 +1137,14 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         }
     }
     // the running frames' RGBA8 thresholds for this gamma (exact bytes without a binary64 pow: preview_kernel)
-    const GammaTable* thresholds = nullptr;
+    GammaSlot* thresholds = nullptr;
     if (want_preview) {
         HIP_TRY(hipSetDevice(h.device));
-        thresholds = gamma_table(sc, s->gamma, h.stream);
+        thresholds = gamma_table(sc, s->gamma);
     }
     sc->ckpt_pixels = n;
     sc->ckpt_done = s0;
+    sc->ckpt_key = ckpt_key(s, cw, ch);
     ctl_store(sc->ctl, kCtlStop, 0);
     ctl_store(sc->ctl, kCtlDone, (uint32_t)s0);
 
@@ -1208,7 +1279,9 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
             // hipMemcpyAsync here is a blit kernel that waits for wave slots behind the trace waves
             // (measured 7-15 ms per 8-MB frame while batches overlap)
             FinalizeParams fp{(int)n, be - base, s->tone_map, s->exposure, s->gamma};
-            HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview_dev[kb % ring], h.stream, thresholds));
+            HIP_TRY(launch_finalize(fp, h.sum.p, nullptr, nullptr, sc->preview_dev[kb % ring], h.stream,
+                                    thresholds ? thresholds->table() : nullptr));
+            if (thresholds) HIP_TRY(gamma_used(thresholds, h.stream));
         }
         HIP_TRY(hipEventRecord(sc->batch_done[kb % ring], h.stream));
         return RT_OK;
@@ -1398,6 +1471,9 @@ int rt_render_resume(rt_scene* sc, const rt_settings* s, const double* sums, int
         if (sc->ckpt_pixels == 0 || sc->ckpt_pixels != (size_t)cw * ch || samples_done != sc->ckpt_done)
             return fail(RT_ERR_INVALID, "no resident checkpoint of %d samples over %d x %d pixels (sums NULL)",
                         samples_done, cw, ch);
+        if (!(sc->ckpt_key == ckpt_key(s, cw, ch)))
+            return fail(RT_ERR_INVALID, "the resident checkpoint is of another frame, crop, sample_begin, precision, "
+                        "seed, aa_mode or max_depth (sums NULL)");
         return render_impl(sc, s, out, progress, user, stats, nullptr, samples_done, true);
     }
     return render_impl(sc, s, out, progress, user, stats, sums, samples_done);

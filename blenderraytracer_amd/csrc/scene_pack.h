@@ -305,10 +305,14 @@ struct BvhBuilder {
     }
 };
 
-// preorder BvhNode tree -> Bvh2Node array of its inner nodes in preorder (root first); a tree that
-// is a single leaf becomes one node whose second child is an empty leaf.  (Breadth-first order with
-// the top levels staged in LDS measured no faster: the node loads hit L1/L2, DESIGN.md "BVH".)
-inline std::vector<Bvh2Node> make_wide(const std::vector<BvhNode>& t) {
+// preorder BvhNode tree -> Bvh2Node array of its inner nodes (root first); a tree that is a single leaf
+// becomes one node whose second child is an empty leaf.  The first `top` inner nodes in breadth-first
+// order come first (indices [0, top): the tree's top levels, which trace_pool_lds_kernel's triangle walk
+// copies into LDS, ACC_BVH_TRI_LDS), the rest follow in preorder (a subtree's nodes stay close in
+// memory).  A permutation of the nodes only: every walk visits the same children in the same order.
+// (Round 1: breadth-first top levels staged in LDS by one-wave workgroups measured slower — the copy was
+// paid per item; round 4: the layout alone measured +-1.5 %, noise.)  RT_TRI_TOP_NODES: pt_core.h
+inline std::vector<Bvh2Node> make_wide(const std::vector<BvhNode>& t, int top = 0) {
     std::vector<Bvh2Node> out;
     if (t.empty()) return out;
     auto box = [&](Bvh2Node& n, int k, int i) {    // child k's bounds = tree node i's
@@ -325,8 +329,18 @@ inline std::vector<Bvh2Node> make_wide(const std::vector<BvhNode>& t) {
     }
     std::vector<int> map(t.size(), -1);
     int k = 0;
-    for (size_t i = 0; i < t.size(); ++i)           // preorder: a subtree's nodes stay close in memory
-        if (t[i].fc == 0) map[i] = k++;
+    if (top > 0) {                                  // breadth-first: root, its inner children, ...
+        std::vector<int> q{0};
+        for (size_t h = 0; h < q.size() && k < top; ++h) {
+            const int i = q[h];
+            map[i] = k++;
+            const int l = i + 1, r = t[l].skip;
+            if (t[l].fc == 0) q.push_back(l);
+            if (t[r].fc == 0) q.push_back(r);
+        }
+    }
+    for (size_t i = 0; i < t.size(); ++i)           // the rest in preorder
+        if (t[i].fc == 0 && map[i] < 0) map[i] = k++;
     out.resize(k);
     auto ref = [&](int i) { return t[i].fc ? ~t[i].fc : map[i]; };
     for (size_t i = 0; i < t.size(); ++i) {
@@ -513,7 +527,7 @@ inline void build_bvhs(HostScene& hs) {
     hs.tri_bvh = std::move(tb.nodes);
     hs.tri_bvh_prims = std::move(tb.order);
     hs.sphere_wide = make_wide(hs.sphere_bvh);
-    hs.tri_wide = make_wide(hs.tri_bvh);
+    hs.tri_wide = make_wide(hs.tri_bvh, RT_TRI_TOP_NODES);
 }
 
 // The binary32 pre-filter record of a triangle {v0, e1, e2, ...} (binary64, pt_core.h tri_filter_bound):

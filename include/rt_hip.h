@@ -237,10 +237,13 @@ void rt_scene_destroy(rt_scene* scene);
  * thread.  Batches are pipelined: on one device (up to 64 batches whose partials fit RT_FUSED_MB) all
  * of them are traced by ONE launch and each batch is added as soon as its last item is done; otherwise
  * up to 3 per device are queued on the GPU beyond the one the host waits for.  With the sample pool and
- * several batches a cancel stops the batches within a few 8x8 tile x sample-chunk items (the LDS pool
- * kernel checks every 4th item of each wave: a few milliseconds on config 3) and the render returns
- * once the GPU has drained; the checkpoint holds the batches fully added before that.  Otherwise (sample order, one
- * batch, partials that do not fit) it is observed between batches and the queued ones complete.
+ * several batches a cancel stops the batches at their next 8x8 tile x sample-chunk item: the persistent
+ * (LDS) pool launches read no cancel word — rt_cancel moves each in-flight launch's work queue past its
+ * last item from a high-priority stream, so every wave's next take ends its loop and only the items
+ * already taken finish (about 7 ms to return on config 3) — and the one-wave pool kernel's workgroups
+ * read the cancel word as they start.  The render returns once the GPU has drained; the checkpoint holds
+ * the batches fully added before that.  Otherwise (sample order, one batch, partials that do not fit)
+ * it is observed between batches and the queued ones complete.
  * RT_ERR_CANCELLED unless every sample was traced.
  * Threading: one call in flight per scene (rt_render, rt_render_resume, rt_trace_device,
  * rt_finalize_device, rt_render_checkpoint), as for the reference's render(); calls on different
@@ -260,7 +263,9 @@ int rt_render(rt_scene* scene, const rt_settings* settings, const rt_output* out
  * Resident checkpoints (no host copy of the sums): rt_render_checkpoint(scene, NULL, 0, &done)
  * returns only samples_done, and rt_render_resume(..., sums = NULL, samples_done, ...) continues from
  * the sums the scene still holds on its device — valid until the scene's next render (the call fails
- * with RT_ERR_INVALID unless samples_done and the crop's pixel count are the checkpoint's). */
+ * with RT_ERR_INVALID unless samples_done, the frame size, the crop window, sample_begin, precision,
+ * seed, aa_mode and max_depth are the checkpoint's; a render that fails before its sums are consistent
+ * leaves no checkpoint). */
 int rt_render_checkpoint(rt_scene* scene, double* sums, size_t count, int32_t* samples_done);
 int rt_render_resume(rt_scene* scene, const rt_settings* settings, const double* sums, int32_t samples_done,
                      const rt_output* out, rt_progress_fn progress, void* user, rt_stats* stats);

@@ -276,6 +276,76 @@ def test_resume_with_one_batch_left_is_bit_exact(gpu):
     rt2.close()
 
 
+def test_resident_resume_checks_its_checkpoint(gpu):
+    """rt_render_resume(sums = NULL) continues from the sums left on the device only for the checkpoint's
+    own frame, crop, first sample, precision and seed (the pixel count alone let a crop of the
+    same area at another origin continue from unrelated sums); the matching resume is bit-exact."""
+    rt = _rtow(64, 48, 16)
+    lib = capi.load_library()
+    scene = rt.scene_handle()
+    crop = (0, 0, 32, 24)
+    full = rt.render(want=("mean",), crop=crop, batch_samples=4)["mean"]
+    with pytest.raises(RuntimeError, match="CANCELLED"):
+        rt.render(crop=crop, batch_samples=4, on_progress=lambda f: True)
+    done = C.c_int32()
+    capi.check(lib.rt_render_checkpoint(scene, None, 0, C.byref(done)))
+    assert 4 <= done.value < 16
+    mean = np.zeros((24, 32, 3))
+    out = capi.Output()
+    out.mean = mean.ctypes.data_as(C.POINTER(C.c_double))
+
+    def resume(st):
+        return lib.rt_render_resume(scene, C.byref(st), None, done.value, C.byref(out), capi.PROGRESS_FN(0), None,
+                                    None)
+    other_origin = rt.settings(crop=(8, 0, 32, 24), batch_samples=4)          # same area, another window
+    assert resume(other_origin) == -1 and "another frame" in lib.rt_last_error().decode()
+    other_seed = rt.settings(crop=crop, batch_samples=4)
+    other_seed.seed += 1
+    assert resume(other_seed) == -1
+    other_prec = rt.settings(crop=crop, batch_samples=4)
+    other_prec.precision = capi.RT_PREC_F32
+    assert resume(other_prec) == -1
+    capi.check(resume(rt.settings(crop=crop, batch_samples=4)))                # the checkpoint's own: resumes
+    assert np.array_equal(mean, full)
+    rt.close()
+
+
+def test_finalize_two_streams_two_gammas(gpu):
+    """Two asynchronous RGBA8-only rt_finalize_device calls with different gammas on two streams, no host
+    wait in between (one gamma table per scene was rebuilt in place for the second call while
+    the first call's kernel could still read it): each frame equals its own synchronous finalize_kernel
+    frame (Float32 output requested, so the table is not used)."""
+    import torch
+    rng = np.random.default_rng(5)
+    n = 1 << 18
+    sums = torch.from_numpy(rng.uniform(0.0, 1.5, 3 * n)).cuda()
+    rt = _rtow(n, 1, 1, seed=1)
+    lib = capi.load_library()
+    scene = rt.scene_handle()
+    gammas = (2.2, 1.7, 2.2, 0.8)
+    refs = []
+    for g in gammas:
+        rt.gamma = g
+        ref = torch.zeros(4 * n, dtype=torch.uint8, device="cuda")
+        post = torch.zeros(4 * n, dtype=torch.float32, device="cuda")
+        capi.check(lib.rt_finalize_device(scene, C.byref(rt.settings()), C.c_void_p(sums.data_ptr()), None,
+                                          C.c_void_p(post.data_ptr()), C.c_void_p(ref.data_ptr()), None))
+        refs.append(ref)
+    torch.cuda.synchronize()
+    for rep in range(3):
+        streams = [torch.cuda.Stream() for _ in gammas]
+        outs = [torch.zeros(4 * n, dtype=torch.uint8, device="cuda") for _ in gammas]
+        torch.cuda.synchronize()
+        for g, st, o in zip(gammas, streams, outs):
+            rt.gamma = g
+            capi.check(lib.rt_finalize_device(scene, C.byref(rt.settings()), C.c_void_p(sums.data_ptr()), None, None,
+                                              C.c_void_p(o.data_ptr()), C.c_void_p(st.cuda_stream)))
+        torch.cuda.synchronize()
+        for g, o, r in zip(gammas, outs, refs):
+            assert torch.equal(o, r), (rep, g)
+    rt.close()
+
+
 def test_checkpoint_resume_is_bit_exact(gpu):
     """Progressive rendering: cancel after some batches, checkpoint the float64 sums,
     resume in a NEW scene handle from the saved state: identical bits to an uninterrupted render with
@@ -650,6 +720,76 @@ def test_cancel_one_of_two_concurrent_renders(gpu, tmp_path):
     assert bool(r["a_resume_equal"])
 
 
+_QUEUES_SCRIPT = r'''
+import sys, threading, time, ctypes as C
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+import torch
+from blenderraytracer_amd import capi
+from blenderraytracer_amd.renderer import GpuRayTracer
+from blenderraytracer_amd.scene import load_scene_json
+def tracer(w, h, spp, seed):
+    rt = GpuRayTracer(w, h, seed=seed)
+    assert rt.load_from_json(load_scene_json("rtow.json"))
+    rt.update_render_settings({"maxBounces": 5, "samples": spp})
+    return rt
+lib = capi.load_library()
+big, small = tracer(3840, 2160, 512, 7), tracer(32, 32, 2, 9)
+assert lib.rt_scene_walk(small.scene_handle(), capi.RT_PREC_F64, 0) == 2      # the grid: LDS pool launches
+ref_big = big.render(want=("mean",))["mean"]
+n, N = 32 * 32, int(sys.argv[3])
+st = small.settings()
+one = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
+torch.cuda.synchronize()
+capi.check(lib.rt_trace_device(small.scene_handle(), C.byref(st), C.c_void_p(one.data_ptr()), None, 1, None))
+ref_small = one.cpu().numpy()
+bufs = torch.zeros((N, 3 * n), dtype=torch.float64, device="cuda")
+side = torch.cuda.Stream()
+torch.cuda.synchronize()
+box = {}
+def long_render():
+    box["big"] = big.render(want=("mean",))["mean"]
+    box["t"] = time.perf_counter()
+th = threading.Thread(target=long_render)
+th.start()
+time.sleep(0.02)
+enq = []
+for k in range(N):              # every call enqueues one LDS pool launch on `side`, no host wait
+    capi.check(lib.rt_trace_device(small.scene_handle(), C.byref(st), C.c_void_p(bufs[k].data_ptr()),
+                                   C.c_void_p(side.cuda_stream), 0, None))
+    enq.append(time.perf_counter())
+th.join()
+torch.cuda.synchronize()
+out = bufs.cpu().numpy()
+bad = sum(not np.array_equal(out[k], ref_small) for k in range(N))
+during = sum(t < box["t"] for t in enq)
+print(f"{during} of {N} small launches enqueued while the long render ran; {bad} differ", file=sys.stderr)
+np.savez(sys.argv[2], big_equal=np.array_equal(box["big"], ref_big), bad=bad, during=during)
+'''
+
+
+def test_lds_queues_owned_under_concurrent_launches(gpu, tmp_path):
+    """VERDICT r5 item 1: every LDS pool launch holds a work queue of its own (queue_slots.h).  One long
+    render (RTOW 4K x 512 spp, one LDS launch) runs on one thread while another enqueues 2048 small
+    LDS-pool launches of another scene (rt_trace_device, asynchronous, on a side stream) — twice the
+    1024 queue pairs, so round 5's ring handed the long launch's pair to a small one.  Both the long
+    render and every small one are bit-identical to their solo renders."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", _QUEUES_SCRIPT, root, str(tmp_path / "q.npz"), "2048"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    print(p.stderr[-400:])
+    r = np.load(tmp_path / "q.npz")
+    # the pairs were (nearly) all held while it ran: with ownership the 1024th acquisition waits for the
+    # long launch's pair; round 5's ring had handed it out instead
+    assert int(r["during"]) >= 1000
+    assert int(r["bad"]) == 0
+    assert bool(r["big_equal"])
+
+
 def test_cancel_latency_triangle_scene(gpu, tmp_path):
     """The same in-batch cancel on config 5 (mesh50k 1920x1080 x 256 spp in four batches): its walk runs
     in the one-wave pool kernel, whose workgroups read the cancel word as their item starts (the LDS
@@ -996,14 +1136,16 @@ def test_overlapped_batches_equal_serial_batches(gpu, tmp_path):
         assert np.array_equal(unfused[k], ref, equal_nan=True), k
 
 
-@pytest.mark.parametrize("gamma", [2.2, 1.0, 0.45, 3.7])
+@pytest.mark.parametrize("gamma", [2.2, 1.0, 0.45, 3.7, 0.25, 4.0, 50.0])
 def test_preview_thresholds_match_finalize(gpu, gamma):
     """preview_kernel's RGBA8 bytes (the count of gamma thresholds T_k <= tm, T_k computed with the
     device's own binary64 pow) against finalize_kernel's floor(255 pow(max(0, tm), 1/gamma)) on tone-mapped
     values within +-3000 ulps of every threshold (where a non-monotone pow or an off-by-one search would
     show), plus random, negative, zero, huge, infinite and NaN values: rt_finalize_device with RGBA8 only
     takes the threshold kernel, with the Float32 frame requested too finalize_kernel (linear tone map,
-    exposure 1, one sample: tm = the sum)."""
+    exposure 1, one sample: tm = the sum).  0.25 and 4.0 are the ends of the range whose tables are used
+    (kGammaMin / kGammaMax, pt_launch.h); gamma 50 lies outside it, so both calls take finalize_kernel
+    (a non-monotone region wider than the exception scan would otherwise go unseen)."""
     import torch
     k = np.arange(1, 256, dtype=np.float64)
     approx = (k / 255.0) ** gamma                                  # T_k up to a few ulps
