@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks on fewer GPUs (rank -> device LOCAL_RANK %% device count, sums "
                          "reduced through host memory); never a measurement")
+    ap.add_argument("--bands", type=int, default=None,
+                    help="ranks mode: reduce the sums band by band while the later bands trace "
+                         "(rt_trace_device_bands); default 8 when several ranks reduce, else 0")
     ap.add_argument("--dump", help="rank 0 writes the frame's float64 sums and RGBA8 here (.npz) after the timed steps")
     return ap.parse_args()
 
@@ -401,7 +404,8 @@ def main():
         from blenderraytracer_amd.distributed import InProcessRender
         job = InProcessRender(rt, inproc_devices)
     else:
-        job = ShardedRender(rt, rank=rank, world=world, device=torch.device("cuda", local))
+        bands = args.bands if args.bands is not None else (8 if world > 1 else 0)
+        job = ShardedRender(rt, rank=rank, world=world, device=torch.device("cuda", local), bands=bands)
     for _ in range(args.warmup):
         job.step()
     torch.cuda.synchronize()
@@ -586,7 +590,8 @@ def main():
             "prim_tests_per_segment": round((sph + tri) / seg_launch, 3) if bvh else None})
         if distributed:
             mp_mode = {"mode": "ranks", "world_size": dist.get_world_size(), "backend": dist.get_backend(),
-                       "launcher": "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else "bench.py spawn"}
+                       "launcher": "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else "bench.py spawn",
+                       "reduce_bands": job.bands}
             parallelism = (f"sample-split x{world} + RCCL reduce" if args.dist_backend == "nccl" and world > 1 else
                            "1 GPU, RCCL reduce at world size 1" if args.dist_backend == "nccl" else
                            f"REHEARSAL sample-split x{world} over {ndev} GPU(s), gloo host reduce: not a measurement")

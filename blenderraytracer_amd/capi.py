@@ -75,6 +75,7 @@ class Stats(C.Structure):
 
 
 PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.c_double, C.c_void_p)
+BAND_FN = C.CFUNCTYPE(C.c_int, C.c_int32, C.c_int32, C.c_int32, C.c_void_p)   # rt_band_fn
 
 # every symbol include/rt_hip.h declares (checked by tests/test_capi_symbols.py)
 EXPORTS = {
@@ -87,6 +88,8 @@ EXPORTS = {
                             C.POINTER(Stats)]),
     "rt_trace_device": (C.c_int, [C.c_void_p, C.POINTER(Settings), C.c_void_p, C.c_void_p, C.c_int,
                                   C.POINTER(Stats)]),
+    "rt_trace_device_bands": (C.c_int, [C.c_void_p, C.POINTER(Settings), C.c_void_p, C.c_void_p, C.c_int32, BAND_FN,
+                                        C.c_void_p, C.POINTER(Stats)]),
     "rt_finalize_device": (C.c_int, [C.c_void_p, C.POINTER(Settings), C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p]),
     "rt_cancel": (C.c_int, [C.c_void_p]),

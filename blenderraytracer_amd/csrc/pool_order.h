@@ -59,9 +59,45 @@ RT_HD unsigned pool_position(unsigned b, unsigned n) {
         return g * 8 * K + (r & 7) * K + (r >> 3);
     }
 }
+// Band-major order (ImageParams::bands = B > 0, rt_trace_device_bands): the crop's tile rows split into B
+// horizontal bands (band b: tile rows [b T / B, (b + 1) T / B), T tile rows), all items of band b — its
+// tiles x the launch's band_chunks chunks, chunk-major inside the band — before any of band b + 1, so the
+// bands' pixels become final one after another and each can be reduced across GPUs while the later bands
+// trace.  A permutation only: every item is traced as before, its partials stay at
+// chunk * tiles + tile, and the reduce adds each pixel's chunks in chunk order (bit-identical sums).
+RT_HD int band_row0(const ImageParams& im, int b) {
+    return (int)((long long)b * ((im.ch + 7) / 8) / im.bands);
+}
+RT_HD unsigned band_item(const ImageParams& im, unsigned p, int tiles) {
+    const int tiles_x = (im.cw + 7) / 8;
+    const unsigned chunks = (unsigned)im.band_chunks;
+    for (int b = 0; b < im.bands; ++b) {
+        const int r0 = band_row0(im, b), r1 = band_row0(im, b + 1);
+        const unsigned n = (unsigned)((r1 - r0) * tiles_x);
+        if (p < n * chunks) {
+            const unsigned ci = p / n;
+            return ci * (unsigned)tiles + (unsigned)(r0 * tiles_x) + (p - ci * n);
+        }
+        p -= n * chunks;
+    }
+    return p;   // positions beyond the items (not taken)
+}
+// band of tile `tile` and the items that complete it
+RT_HD int band_of_tile(const ImageParams& im, int tile) {
+    const int row = tile / ((im.cw + 7) / 8);
+    int b = (int)((long long)row * im.bands / ((im.ch + 7) / 8));
+    while (b > 0 && band_row0(im, b) > row) --b;            // floor division's neighbours
+    while (b + 1 < im.bands && band_row0(im, b + 1) <= row) ++b;
+    return b;
+}
+RT_HD uint32_t band_items(const ImageParams& im, int b) {
+    return (uint32_t)((band_row0(im, b + 1) - band_row0(im, b)) * ((im.cw + 7) / 8)) * (uint32_t)im.band_chunks;
+}
+
 // item (chunk * tiles + tile) at position p of the visiting order.  (A longest-first order of each
 // chunk's tiles, from a host estimate of the frame's cost, measured slower in round 5: DESIGN.md §4.)
 RT_HD unsigned item_at(const ImageParams& im, unsigned p, int tiles) {
+    if (im.bands > 0) return band_item(im, p, tiles);
     if constexpr (RT_TILE_BLOCK <= 1) return p;
     const unsigned ci = p / (unsigned)tiles;
     return ci * (unsigned)tiles + (unsigned)tile_at(im, (int)(p - ci * (unsigned)tiles));

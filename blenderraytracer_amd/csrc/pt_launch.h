@@ -31,6 +31,14 @@ struct Counters {
     // all of them: the waves' reads spread over many lines instead of queueing on one
     const uint32_t* cancel = nullptr;
     uint32_t* aborted = nullptr;
+    // what the one-wave pool kernel actually reads: a copy of the cancel word in device memory
+    // (kDevCancelCopies words, one per 128-B line), set to cancel_gen by cancel_pool_launches from a
+    // high-priority stream — an L2 hit instead of a read over PCIe per workgroup (mesh50k cancel 25 ms ->
+    // DESIGN.md §1).  cancel_gen: the render's generation, so a set left over from an earlier render of
+    // the scene never matches.  A fused launch's skipping workgroups leave `aborted` alone (its batches
+    // are committed by their flags)
+    const uint32_t* cancel_dev = nullptr;
+    uint32_t cancel_gen = 0;
     // fused batches (launch_trace_batches): per batch, the items done (device memory, zeroed before the
     // launch) and the flag the item completing the batch raises (mapped host memory: the host enqueues
     // the batch's reduce once it is set, and its gate commits the batch only if it is set)
@@ -38,6 +46,7 @@ struct Counters {
     uint32_t* batch_flag = nullptr;      // batch b's flag: batch_flag[b * ImageParams::batch_ways]
 };
 constexpr int kCancelCopies = 128, kCancelStride = 32;
+constexpr int kDevCancelCopies = 16;      // device-memory copies (Counters::cancel_dev)
 
 // The commit of one batch's chunk partials (render_impl with a cancel word): a one-thread gate kernel
 // before the reduce reads the batch's `aborted` word and the render's sticky `stop` word (both mapped
@@ -89,6 +98,21 @@ hipError_t launch_trace_batches(const SceneView<R>& sc, const ImageParams& im, c
 // device is kept.  A launch cancelled after all its items were taken still counts as aborted.
 hipError_t cancel_pool_launches(const uint32_t* cancel);
 void forget_pool_launches(const uint32_t* cancel);
+// the device-memory cancel word (Counters::cancel_dev) of one device of a render registered under its host
+// cancel word: cancel_pool_launches(cancel) writes `gen` into it (a one-thread kernel on the device's
+// high-priority stream); forget_pool_launches(cancel) drops the registration
+void register_cancel_word(const uint32_t* cancel, int device, uint32_t* word, uint32_t gen);
+
+// One launch with its items band-major over `bands` horizontal bands of whole tile rows (pool_order.h
+// band_item): every chunk's partials into `part` (>= plan.part_bytes, even for one chunk), band b's items
+// counted in c.batch_count[b] and its flag c.batch_flag[b] raised when they are all done.  The same items,
+// chunk and partials as launch_trace of the same samples, so reducing every band's tiles
+// (launch_reduce_tiles) gives the same sums bit for bit.  plan: the launch's pool plan (out)
+template <class R>
+hipError_t launch_trace_bands(const SceneView<R>& sc, const ImageParams& im, const Counters& c, bool bvh, int bands,
+                              double* part, size_t part_bytes, PoolPlan* plan, hipStream_t stream);
+hipError_t launch_reduce_tiles(const ImageParams& im, double* sum, const double* part, int tiles, int chunks,
+                               int tile0, int ntiles, hipStream_t stream, const ReduceGate* gate = nullptr);
 
 // doubles of one batch's partials in a fused launch, and the items that complete it
 size_t fused_batch_doubles(int cw, int ch, int batch, bool tri_bvh, int chunk);

@@ -29,6 +29,10 @@ struct ImageParams {
     // of the render (batch b starts batch_ways * batch_samples samples after batch b - 1, and raises the
     // flag batch_flag[b * batch_ways]); 0 or 1: consecutive batches
     int batch_ways;
+    // pixel bands (rt_trace_device_bands, pool_order.h band_item): the launch's items band-major over `bands`
+    // horizontal bands of whole tile rows, band_chunks chunks each; band b's items counted in
+    // Counters::batch_count[b], its flag raised when all are done; 0: no bands
+    int bands, band_chunks;
 };
 
 // Stochastic AA offsets (ray-tracer.js:136-141): sqrt, cos and sin in binary64 are long code that

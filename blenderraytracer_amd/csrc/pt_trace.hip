@@ -127,12 +127,14 @@ __device__ __forceinline__ void add_totals(const Counters& c, const PixelResult&
 // cancel word at all (cancel_pool_launches moves its queue instead: a poll inside its item loop, even
 // one read per 16 queue positions, cost config 3's 16 fused batches 3-5 % through the kernel's
 // register allocation).
-// copy: the wave's copy of the word (Counters::cancel); one line read by every wave measured 50 us per
-// read (RTOW 16 progressive batches: +4.5 % kernel time), the reads of one line being serialized
+// copy: the wave's copy of the word; one line read by every wave measured 50 us per read (RTOW 16
+// progressive batches: +4.5 % kernel time), the reads of one line being serialized.  Round 6: the copy in
+// device memory (Counters::cancel_dev, agent scope: an L2 read) instead of the host word (system scope: a
+// read over PCIe per workgroup, which bounded how fast a cancelled launch's remaining workgroups drain)
 __device__ __forceinline__ bool cancel_requested(const Counters& c, unsigned copy) {
-    return RT_CANCEL_POLL && c.cancel &&
-           __hip_atomic_load(const_cast<uint32_t*>(c.cancel) + (copy % kCancelCopies) * kCancelStride, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    return RT_CANCEL_POLL && c.cancel_dev &&
+           __hip_atomic_load(const_cast<uint32_t*>(c.cancel_dev) + (copy % kDevCancelCopies) * kCancelStride,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == c.cancel_gen;
 }
 // this batch leaves items untraced: its partials must not be reduced (one lane writes; a fused launch's
 // batches are committed by their completion flags instead, ReduceGate::complete)
@@ -302,7 +304,9 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
     __syncthreads();
     if constexpr (CANCEL) {
         if (__builtin_amdgcn_readfirstlane((int)cancel_requested(args.c, blockIdx.x))) {
-            if (lane == 0) mark_aborted(args.c);  // the workgroup is one item: it is left untraced
+            // the workgroup is one item: it is left untraced (a fused launch's batch then never raises
+            // its flag; a per-batch launch's gate reads `aborted`)
+            if (lane == 0 && !args.c.batch_count) mark_aborted(args.c);
             return;
         }
     }
@@ -411,7 +415,14 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
             args.c.sum[3 * qq + 2] += acc[128 + lane];
         }
     }
-    if (args.c.batch_count) item_done(args.c, cr.b, (uint32_t)(im.batch_chunks * tiles), im.batch_ways, lane);
+    if (args.c.batch_count) {
+        if (im.bands) {
+            const int bb = band_of_tile(im, tile);
+            item_done(args.c, bb, band_items(im, bb), 1, lane);
+        } else {
+            item_done(args.c, cr.b, (uint32_t)(im.batch_chunks * tiles), im.batch_ways, lane);
+        }
+    }
     add_totals<ACC>(args.c, res, lane);
 }
 
@@ -515,7 +526,14 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
             args.c.sum[3 * qq + 2] += acc[128 + lane];
         }
     }
-    if (args.c.batch_count) item_done(args.c, cr.b, (uint32_t)(im.batch_chunks * tiles), im.batch_ways, lane);
+    if (args.c.batch_count) {
+        if (im.bands) {
+            const int bb = band_of_tile(im, tile);
+            item_done(args.c, bb, band_items(im, bb), 1, lane);
+        } else {
+            item_done(args.c, cr.b, (uint32_t)(im.batch_chunks * tiles), im.batch_ways, lane);
+        }
+    }
     acc[lane] = 0;                            // the wave's next item starts from zero partials
     acc[64 + lane] = 0;
     acc[128 + lane] = 0;
@@ -673,8 +691,9 @@ static_assert(std::is_same<FirstParam<decltype(&trace_pool_lds_kernel<float, fal
 // workgroup waits for four free wave slots on one CU and was measured to take 7.8 ms instead of 0.1.
 __global__ __launch_bounds__(64) void reduce_kernel(const ImageParams im, double* __restrict__ sum,
                                                     const double* __restrict__ part, const int tiles,
-                                                    const int chunks, const uint32_t* __restrict__ skip) {
-    const int tile = blockIdx.x, m = threadIdx.x;
+                                                    const int chunks, const uint32_t* __restrict__ skip,
+                                                    const int tile0 = 0) {
+    const int tile = tile0 + (int)blockIdx.x, m = threadIdx.x;
     if (tile >= tiles || (skip && *skip)) return;
     const Tile t = tile_of(im, tile);
     if (m >= t.nv) return;
@@ -852,9 +871,14 @@ static size_t lds_nodes_bytes(const SceneView<R>& sc) {
 }
 
 // Which launches of scenes with a triangle tree run trace_pool_lds_kernel<.., ACC_BVH_TRI_LDS> (the top
-// levels of the triangle tree in LDS): RT_LDS_TRI = 0 never, 1 (default) binary64, 2 both precisions.
+// levels of the triangle tree in LDS): RT_LDS_TRI = 0 (default) never, 1 binary64, 2 both precisions.
+// Measured (round 6, mesh50k 1080p x 128 spp f64, interleaved x2, identical images): the one-wave kernel
+// 6915 / 6845 Msamples/s; the persistent kernel with 1019 / 255 / 64 top nodes in LDS 6360-6369 /
+// 6319-6323 / 6238-6272, in 8-wave workgroups (507 nodes, two copies per CU) 6283-6336: the LDS nodes buy
+// +1.8 % over the same kernel without them, the persistent form loses 9 % against hardware-dispatched
+// one-wave workgroups (round 5's persistent one-wave kernel with per-XCD queues: -10 %) — DESIGN.md §4
 #ifndef RT_LDS_TRI
-#define RT_LDS_TRI 1
+#define RT_LDS_TRI 0
 #endif
 // the triangle-tree nodes a launch stages (0: the one-wave kernel): as many of the breadth-first prefix
 // (RT_TRI_TOP_NODES, or RT_TRI_LDS_NODES from the environment for A/B runs) as fit the CU's LDS beside
@@ -963,6 +987,11 @@ __global__ __launch_bounds__(64) void queue_cancel_kernel(const int qi, const ui
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope
     __hip_atomic_fetch_max(g_pool_queue + 2 * qi, items, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// a render's device-memory cancel word (Counters::cancel_dev): every copy := gen
+__global__ __launch_bounds__(64) void cancel_word_kernel(uint32_t* word, const uint32_t gen) {
+    if (threadIdx.x < kDevCancelCopies)
+        __hip_atomic_store(word + threadIdx.x * kCancelStride, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // after the launch (and the move) ended: the queue pair back to 0 for its next holder
 __global__ __launch_bounds__(64) void queue_clear_kernel(const int qi) {
     if (threadIdx.x < 2) __hip_atomic_store(g_pool_queue + 2 * qi + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -979,6 +1008,25 @@ struct PoolLaunch {
 };
 std::vector<PoolLaunch> g_launches;       // launches that may still run (pruned as they are found done)
 hipStream_t g_cancel_stream[64];          // per device, created on first use (under g_launch_mu)
+struct CancelWord {
+    const uint32_t* cancel;
+    int device;
+    uint32_t* word;
+    uint32_t gen;
+};
+std::vector<CancelWord> g_words;          // registered device cancel words (until forget_pool_launches)
+
+hipError_t cancel_stream(int device, hipStream_t* out) {   // under g_launch_mu, device current
+    hipStream_t& cs = g_cancel_stream[device & 63];
+    hipError_t e = hipSuccess;
+    if (!cs) {
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        e = hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, hi);
+    }
+    *out = cs;
+    return e;
+}
 
 // drop the records for which keep() is false
 template <class F>
@@ -1016,12 +1064,8 @@ hipError_t cancel_pool_launches(const uint32_t* cancel) {
         if (launch_done(l)) return false;
         if (cur < 0 && hipGetDevice(&cur) != hipSuccess) cur = 0;
         hipError_t e = hipSetDevice(l.device);
-        hipStream_t& cs = g_cancel_stream[l.device & 63];
-        if (e == hipSuccess && !cs) {
-            int lo = 0, hi = 0;
-            (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-            e = hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, hi);
-        }
+        hipStream_t cs = nullptr;
+        if (e == hipSuccess) e = cancel_stream(l.device, &cs);
         hipEvent_t ev = nullptr;
         if (e == hipSuccess) {
             hipLaunchKernelGGL(queue_cancel_kernel, dim3(1), dim3(64), 0, cs, l.qi, l.items, l.aborted);
@@ -1044,6 +1088,18 @@ hipError_t cancel_pool_launches(const uint32_t* cancel) {
         if (e != hipSuccess && err == hipSuccess) err = e;
         return false;                     // cancelled: the record goes
     });
+    for (const CancelWord& w : g_words) { // the one-wave kernels' device words
+        if (w.cancel != cancel) continue;
+        if (cur < 0 && hipGetDevice(&cur) != hipSuccess) cur = 0;
+        hipError_t e = hipSetDevice(w.device);
+        hipStream_t cs = nullptr;
+        if (e == hipSuccess) e = cancel_stream(w.device, &cs);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(cancel_word_kernel, dim3(1), dim3(64), 0, cs, w.word, w.gen);
+            e = hipGetLastError();
+        }
+        if (e != hipSuccess && err == hipSuccess) err = e;
+    }
     if (cur >= 0) (void)hipSetDevice(cur);
     return err;
 }
@@ -1051,6 +1107,15 @@ hipError_t cancel_pool_launches(const uint32_t* cancel) {
 void forget_pool_launches(const uint32_t* cancel) {
     std::lock_guard<std::mutex> g(g_launch_mu);
     prune_launches([&](const PoolLaunch& l) { return l.cancel != cancel && !launch_done(l); });
+    size_t w = 0;
+    for (size_t k = 0; k < g_words.size(); ++k)
+        if (g_words[k].cancel != cancel) g_words[w++] = g_words[k];
+    g_words.resize(w);
+}
+
+void register_cancel_word(const uint32_t* cancel, int device, uint32_t* word, uint32_t gen) {
+    std::lock_guard<std::mutex> g(g_launch_mu);
+    g_words.push_back(CancelWord{cancel, device, word, gen});
 }
 
 static int device_cus() {
@@ -1255,6 +1320,43 @@ template hipError_t launch_trace_batches<double>(const SceneView<double>&, const
                                                  double*, size_t, hipStream_t);
 template hipError_t launch_trace_batches<float>(const SceneView<float>&, const ImageParams&, const Counters&, bool, int,
                                                 double*, size_t, hipStream_t);
+
+// the partials of tiles [tile0, tile0 + ntiles) of a banded launch (launch_trace_bands)
+hipError_t launch_reduce_tiles(const ImageParams& im, double* sum, const double* part, int tiles, int chunks,
+                               int tile0, int ntiles, hipStream_t stream, const ReduceGate* gate) {
+    if (ntiles <= 0) return hipSuccess;
+    if (gate) hipLaunchKernelGGL(reduce_gate_kernel, dim3(1), dim3(64), 0, stream, *gate);
+    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)ntiles), dim3(64), 0, stream, im, sum, part, tiles, chunks,
+                       (const uint32_t*)(gate ? gate->skip : nullptr), tile0);
+    return hipGetLastError();
+}
+
+template <class R>
+hipError_t launch_trace_bands(const SceneView<R>& sc, const ImageParams& im0, const Counters& c, bool bvh, int bands,
+                              double* part, size_t part_bytes, PoolPlan* plan, hipStream_t stream) {
+    if (im0.cw <= 0 || im0.ch <= 0 || im0.s_end <= im0.s_begin || bands <= 0) return hipSuccess;
+    const PoolPlan p = pool_plan(im0.cw, im0.ch, im0.s_end - im0.s_begin, sc.num_tri_nodes > 0, im0.pool_chunk);
+    if (plan) *plan = p;
+    if (!part || !c.batch_count || !c.batch_flag || part_bytes < p.part_bytes || bands > (im0.ch + 7) / 8)
+        return hipErrorInvalidValue;
+    if ((long long)p.tiles * p.chunks > 0x7FFFFFFFLL) return hipErrorInvalidConfiguration;
+    ImageParams im = im0;
+    im.pool_chunk = p.chunk;
+    im.bands = bands;
+    im.band_chunks = p.chunks;
+    TraceArgs<R> a{sc, im, c};
+    const bool count = c.segs || c.draws;
+    if (!bvh) return launch_partials_acc<R, ACC_BRUTE>(a, count, p, part, stream);
+    const int mode = bvh_walk_mode(sc);
+    if (mode == ACC_BVH) return launch_partials_acc<R, ACC_BVH>(a, count, p, part, stream);
+    if (mode == ACC_BVH_SPHERES) return launch_partials_acc<R, ACC_BVH_SPHERES>(a, count, p, part, stream);
+    if (mode == ACC_GRID) return launch_partials_acc<R, ACC_GRID>(a, count, p, part, stream);
+    return launch_partials_acc<R, ACC_BVH_STACK>(a, count, p, part, stream);
+}
+template hipError_t launch_trace_bands<double>(const SceneView<double>&, const ImageParams&, const Counters&, bool, int,
+                                               double*, size_t, PoolPlan*, hipStream_t);
+template hipError_t launch_trace_bands<float>(const SceneView<float>&, const ImageParams&, const Counters&, bool, int,
+                                              double*, size_t, PoolPlan*, hipStream_t);
 
 hipError_t launch_reduce(const ImageParams& im, double* sum, const double* part, bool tri_bvh, hipStream_t stream,
                          const ReduceGate* gate) {

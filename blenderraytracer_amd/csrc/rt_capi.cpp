@@ -20,6 +20,7 @@
 
 #include "../../include/rt_hip.h"
 #include "pt_launch.h"
+#include "pool_order.h"
 #include "scene_pack.h"
 
 using namespace rt;
@@ -202,6 +203,9 @@ struct DeviceState {
     DevBuf<double> fused_part;
     DevBuf<uint32_t> fused_count;
     hipEvent_t fused_done = nullptr;
+    // the one-wave pool kernel's cancel word in device memory (Counters::cancel_dev), zeroed once; each
+    // render matches its own generation
+    DevBuf<uint32_t> cancel_word;
 
     int init(int dev, const HostScene& hs, const rt_scene_desc& d) {
         device = dev;
@@ -223,6 +227,8 @@ struct DeviceState {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&fused_done, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&scratch_ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&copy_ev, hipEventDisableTiming);
+        if (e == hipSuccess) e = cancel_word.ensure((size_t)kDevCancelCopies * kCancelStride);
+        if (e == hipSuccess) e = hipMemset(cancel_word.p, 0, (size_t)kDevCancelCopies * kCancelStride * sizeof(uint32_t));
         if (e != hipSuccess) return fail(RT_ERR_DEVICE, "stream/event create: %s", hipGetErrorString(e));
         return RT_OK;
     }
@@ -237,7 +243,7 @@ struct DeviceState {
         s64.release();
         s32.release();
         sum.release(); segs.release(); draws.release(); total.release(); part.release(); gate_skip.release();
-        fused_part.release(); fused_count.release();
+        fused_part.release(); fused_count.release(); cancel_word.release();
         for (DevBuf<double>& b : part_more) b.release();
         for (hipEvent_t e : {ev[0], ev[1], setup_ev, scratch_ev, copy_ev, fused_done})
             if (e) (void)hipEventDestroy(e);
@@ -354,6 +360,7 @@ struct rt_scene {
     std::vector<GammaSlot> gamma_slots;
     uint64_t gamma_tick = 0;
     std::atomic<int> cancel{0};
+    uint32_t render_gen = 0;        // generation of the current render (device cancel words)
     uint32_t* ctl = nullptr;        // the render's control words (kCtl*), host address
     uint32_t* ctl_dev = nullptr;    // ... their device address (portable mapping: valid on every device)
     size_t ckpt_pixels = 0;         // progressive state of the last rt_render / rt_render_resume:
@@ -938,12 +945,32 @@ int merge_shards(rt_scene* sc, const std::vector<DeviceState*>& states, size_t n
 // the checkpoint is the batches fully reduced by then (`gated`); without overlapped batches it is
 // observed after a batch, and the batches already queued complete.  Several devices: whole batches
 // round-robin (trace_replica), or every batch split over the devices (merge_shards).
-int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_progress_fn progress, void* user,
+// rt_settings.batch_samples = -N: about N progress batches whose size is a multiple of the sample pool's
+// chunk for the render (its rule for the whole sample range [sample_begin, samples), as for one device), so
+// that every batch's items are the one-batch render's items.  Batches of ceil(S / N) samples otherwise cut
+// the chunks: mesh50k (chunk 12) in 16 batches of 16 spp takes one 16-sample chunk per batch, +4 % against
+// one batch.  The resolution depends only on the settings and the scene, so a resume sees
+// the same batches.
+int progress_batch(const rt_scene* sc, const rt_settings* s, int cw, int ch, int steps) {
+    const int base = std::max(0, s->sample_begin);
+    const int end = s->sample_end > 0 ? std::min(s->sample_end, s->samples) : s->samples;
+    const int total = std::max(1, end - base);
+    const int target = std::max(1, (total + steps - 1) / steps);
+    if (!use_pool(s)) return target;
+    const int h = pool_plan(cw, ch, total, sc->tri_bvh).chunk;
+    if (h <= 0 || h >= target) return target;
+    return h * std::max(1, (int)std::lround((double)target / (double)h));
+}
+
+int render_impl(rt_scene* sc, const rt_settings* s_in, const rt_output* out, rt_progress_fn progress, void* user,
                 rt_stats* stats, const double* sums_in, int first, bool resident = false) {
     const double t_start = now_ms();
     if (!sc) return fail(RT_ERR_INVALID, "scene is NULL");
     int cw, ch;
-    int rc = check_settings(s, &cw, &ch);
+    int rc = check_settings(s_in, &cw, &ch);
+    rt_settings s_local = s_in ? *s_in : rt_settings{};
+    if (!rc && s_local.batch_samples < 0) s_local.batch_samples = progress_batch(sc, s_in, cw, ch, -s_local.batch_samples);
+    const rt_settings* s = &s_local;
     if (!rc) rc = check_accel(sc, s);
     if (rc) return rc;
     std::vector<DeviceState*> states;
@@ -958,6 +985,8 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         const uint32_t* word;
         ~LaunchScope() { forget_pool_launches(word); }
     } launch_scope{sc->ctl_dev + kCtlCancel};
+    if (++sc->render_gen == 0) sc->render_gen = 1;   // 0 is the words' initial value
+    for (DeviceState* ds : states) register_cancel_word(sc->ctl_dev + kCtlCancel, ds->device, ds->cancel_word.p, sc->render_gen);
     const size_t n = (size_t)cw * ch;
     const bool want_segs = out && out->segments, want_draws = out && out->draws;
     const bool pool = use_pool(s);
@@ -1072,6 +1101,8 @@ int render_impl(rt_scene* sc, const rt_settings* s, const rt_output* out, rt_pro
         HIP_TRY(hipSetDevice(ds.device));
         Counters& c = cs[k];
         c = Counters{ds.sum.p, nullptr, nullptr, ds.total.p};
+        c.cancel_dev = ds.cancel_word.p;
+        c.cancel_gen = sc->render_gen;
         int b0, b1;
         shard_range(s0, s0 + std::min(batch, s1 - s0), k, nsh, b0, b1);
         const int ns = std::max(1, b1 - b0);
@@ -1518,6 +1549,122 @@ int rt_trace_device(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip
             fill_stats(stats, sc, s, totals, (size_t)cw * ch, im);
             stats->wall_ms = now_ms() - t_start;
         }
+    }
+    return RT_OK;
+}
+
+int rt_trace_device_bands(rt_scene* sc, const rt_settings* s, double* d_sum, void* hip_stream, int32_t bands,
+                          rt_band_fn band_ready, void* user, rt_stats* stats) {
+    const double t_start = now_ms();
+    if (!sc || !d_sum) return fail(RT_ERR_INVALID, "NULL argument");
+    int cw, ch;
+    int rc = check_settings(s, &cw, &ch);
+    if (!rc) rc = check_accel(sc, s);
+    if (rc) return rc;
+    if (s->device_count > 1) return fail(RT_ERR_INVALID, "rt_trace_device_bands traces on the scene's device");
+    const int tile_rows = (ch + 7) / 8;
+    const int nb = std::max(1, std::min({(int)bands, tile_rows, kMaxFused}));
+    ImageParams im = image_params(s, cw, ch);
+    auto deliver_all = [&](int from) -> int {   // bands [from, nb) at once (nothing left to overlap)
+        for (int b = from; b < nb && band_ready; ++b) {
+            im.bands = nb;
+            const int r0 = band_row0(im, b) * 8, r1 = std::min(ch, band_row0(im, b + 1) * 8);
+            if (band_ready(b, r0, r1 - r0, user)) return fail(RT_ERR_CANCELLED, "band_ready stopped at band %d", b);
+        }
+        return RT_OK;
+    };
+    // no pool (sample order) or nothing to trace: rt_trace_device, then every band
+    if (!use_pool(s) || s->max_depth <= 0 || im.s_end <= im.s_begin) {
+        if ((rc = rt_trace_device(sc, s, d_sum, hip_stream, 0, stats))) return rc;
+        return deliver_all(0);
+    }
+    DeviceState& ds = sc->home;
+    HIP_TRY(hipSetDevice(ds.device));
+    hipStream_t st = (hipStream_t)hip_stream;
+    const PoolPlan plan = pool_plan(cw, ch, im.s_end - im.s_begin, sc->tri_bvh, 0);
+    HIP_TRY(ds.total.ensure(kTotalSlots));
+    HIP_TRY(ds.fused_count.ensure((size_t)nb));
+    HIP_TRY(ds.gate_skip.ensure(1));
+    if (ds.part.n * sizeof(double) < plan.part_bytes) {     // every chunk's partials (even one chunk)
+        HIP_TRY(scratch_idle(ds));
+        HIP_TRY(ds.part.ensure(plan.part_bytes / sizeof(double)));
+    }
+    HIP_TRY(order_scratch(ds, st));
+    for (int b = 0; b < nb; ++b) ctl_store(sc->ctl, kCtlFlag + b, 0);
+    ctl_store(sc->ctl, kCtlStop, 0);
+    ctl_store(sc->ctl, kCtlFusedAborted, 0);
+    // the trace runs on the scene's own trace stream, after the caller's work so far (d_sum's zeroing);
+    // the band reduces run on the caller's stream as the bands complete, beside the trace
+    hipStream_t ts = ds.tstream[0];
+    HIP_TRY(hipMemsetAsync(ds.total.p, 0, kTotalSlots * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(ds.fused_count.p, 0, (size_t)nb * sizeof(uint32_t), st));
+    HIP_TRY(hipEventRecord(ds.setup_ev, st));
+    HIP_TRY(hipStreamWaitEvent(ts, ds.setup_ev, 0));
+    Counters c{d_sum, nullptr, nullptr, ds.total.p};
+    c.batch_count = ds.fused_count.p;
+    c.batch_flag = sc->ctl_dev + kCtlFlag;
+    const bool bvh = use_bvh(sc, s);
+    PoolPlan used{};
+    HIP_TRY(hipEventRecord(ds.ev[0], ts));
+    HIP_TRY(s->precision == RT_PREC_F32
+                ? launch_trace_bands<float>(ds.s32.view, im, c, bvh, nb, ds.part.p, ds.part.n * sizeof(double), &used, ts)
+                : launch_trace_bands<double>(ds.s64.view, im, c, bvh, nb, ds.part.p, ds.part.n * sizeof(double), &used, ts));
+    HIP_TRY(hipEventRecord(ds.ev[1], ts));
+    HIP_TRY(hipEventRecord(ds.fused_done, ts));
+    im.bands = nb;
+    im.band_chunks = used.chunks;
+    im.pool_chunk = used.chunk;
+    const int tiles_x = (cw + 7) / 8;
+    int status = RT_OK;
+    for (int b = 0; b < nb && status == RT_OK; ++b) {
+        for (;;) {                                  // band b's items are all done
+            if (ctl_load(sc->ctl, kCtlFlag + b)) break;
+            const hipError_t q = hipEventQuery(ds.fused_done);
+            if (q == hipSuccess) {
+                if (!ctl_load(sc->ctl, kCtlFlag + b)) status = fail(RT_ERR_DEVICE, "band %d was not completed (internal error)", b);
+                break;
+            }
+            if (q != hipErrorNotReady) {
+                (void)hipGetLastError();
+                status = fail(RT_ERR_DEVICE, "band %d: %s", b, hipGetErrorString(q));
+                break;
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+        if (status != RT_OK) break;
+        ReduceGate gate;                            // the acquire end of the band's commit (item_done)
+        gate.aborted = sc->ctl_dev + kCtlFusedAborted;
+        gate.stop = sc->ctl_dev + kCtlStop;
+        gate.done = reinterpret_cast<int32_t*>(sc->ctl_dev + kCtlDone);
+        gate.done_value = 0;
+        gate.skip = ds.gate_skip.p;
+        gate.complete = sc->ctl_dev + kCtlFlag + b;
+        const int r0 = band_row0(im, b), r1 = band_row0(im, b + 1);
+        hipError_t e = launch_reduce_tiles(im, d_sum, ds.part.p, used.tiles, used.chunks, r0 * tiles_x,
+                                           (r1 - r0) * tiles_x, st, &gate);
+        if (e != hipSuccess) { status = fail(RT_ERR_DEVICE, "band reduce: %s", hipGetErrorString(e)); break; }
+        if (band_ready && band_ready(b, r0 * 8, std::min(ch, r1 * 8) - r0 * 8, user))
+            status = fail(RT_ERR_CANCELLED, "band_ready stopped at band %d", b);
+    }
+    // the caller's stream after the whole launch (work totals, and the scratch's next user)
+    HIP_TRY(hipStreamWaitEvent(st, ds.fused_done, 0));
+    unsigned long long totals[kTotalSlots] = {};
+    if (stats) HIP_TRY(hipMemcpyAsync(totals, ds.total.p, sizeof totals, hipMemcpyDeviceToHost, st));
+    HIP_TRY(release_scratch(ds, st));
+    if (status != RT_OK) {
+        const std::string err = g_error;
+        (void)hipStreamSynchronize(st);
+        g_error = err;
+        return status;
+    }
+    if (stats) {
+        HIP_TRY(hipStreamSynchronize(st));
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, ds.ev[0], ds.ev[1]));
+        stats->kernel_ms = ms;
+        stats->finalize_ms = 0;
+        fill_stats(stats, sc, s, totals, (size_t)cw * ch, im);
+        stats->wall_ms = now_ms() - t_start;
     }
     return RT_OK;
 }

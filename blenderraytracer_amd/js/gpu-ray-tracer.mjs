@@ -70,16 +70,16 @@ export function settingsOf(rt, opts = {}) {
 }
 
 // Progress granularity.  The reference reports progress and repaints after every row
-// (ray-tracer.js:224-261); the GPU renders whole frames, so render() splits the samples into
+// (ray-tracer.js:224-261); the GPU renders whole frames, so render() splits the samples into about
 // `progressSteps` batches (default 16; opts.batchSamples overrides, 0 = one batch): after each batch
-// onProgress fires and imageData shows the frame of the samples done so far.
+// onProgress fires and imageData shows the frame of the samples done so far.  The library sizes the
+// batches (rt_settings.batch_samples = -steps) to a multiple of the sample pool's chunk, so progress
+// costs no work-item splits (mesh50k at 256 spp: 22 batches of 12 instead of 16 of 16, DESIGN.md §1).
 export const DEFAULT_PROGRESS_STEPS = 16;
 function batchSamplesOf(rt, opts) {
     if (opts.batchSamples !== undefined) return opts.batchSamples || 0;
     if (!opts.intoImageData) return 0;
-    const samples = rt.antiAliasing === 'none' ? 1 : rt.samples;
-    const steps = opts.progressSteps || DEFAULT_PROGRESS_STEPS;
-    return Math.max(1, Math.ceil(samples / steps));
+    return -(opts.progressSteps || DEFAULT_PROGRESS_STEPS);
 }
 
 const isCancelled = () => typeof window !== 'undefined' && window && window.renderCancelled;

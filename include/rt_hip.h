@@ -152,7 +152,9 @@ typedef struct rt_settings {
     int32_t crop_x0, crop_y0;  /* output window (top-down rows), crop_w/h == 0 -> full image   */
     int32_t crop_w, crop_h;
     int32_t precision;         /* rt_precision */
-    int32_t batch_samples;     /* samples per launch (progress/cancel granularity); 0 = all   */
+    int32_t batch_samples;     /* samples per launch (progress/cancel granularity); 0 = all;
+                                  -N = about N batches, each a multiple of the sample pool's chunk
+                                  (the Node drop-in's default, -16)                               */
     int32_t denoise;           /* this.denoising: PostProcessor.denoise after gamma (ray-tracer.js:266-276);
                                   needs the full frame (crop_w/h = 0 or the whole image) */
     double denoise_weights[2]; /* Math.exp(-1/(2s*s)), Math.exp(-2/(2s*s)), s = denoiseStrength, evaluated by
@@ -277,6 +279,20 @@ int rt_render_resume(rt_scene* scene, const rt_settings* settings, const double*
  * when `sync` is non-zero. */
 int rt_trace_device(rt_scene* scene, const rt_settings* settings, double* d_sum, void* hip_stream,
                     int sync, rt_stats* stats);
+
+/* rt_trace_device with the frame delivered band by band, so a multi-GPU caller can reduce the first
+ * bands across GPUs while the later ones still trace.  The crop's 8-pixel tile rows are
+ * split into `bands` horizontal bands (at most 64 and the tile rows); the trace runs on the scene's own
+ * stream (after the caller's work on `hip_stream` so far) with its work items band-major, and as soon as
+ * band b's items are done its sums are added into d_sum on `hip_stream` and band_ready(b, row0, rows,
+ * user) is called from this thread: the caller may enqueue work on rows [row0, row0 + rows) of d_sum on
+ * hip_stream (or a stream that waits for it), which runs beside the later bands' trace.  A non-zero return
+ * stops the delivery (RT_ERR_CANCELLED; the trace itself completes).  Returns once every band was
+ * delivered and hip_stream has been ordered after the whole trace.  d_sum ends up equal to
+ * rt_trace_device's, bit for bit (same work items, same chunk partials, same order of additions). */
+typedef int (*rt_band_fn)(int32_t band, int32_t row0, int32_t rows, void* user);
+int rt_trace_device_bands(rt_scene* scene, const rt_settings* settings, double* d_sum, void* hip_stream, int32_t bands,
+                          rt_band_fn band_ready, void* user, rt_stats* stats);
 
 /* Epilogue on device: mean = sum / sampleCount, toneMap, gammaCorrect, optional denoise, RGBA8
  * (ray-tracer.js:208-276).  Any output pointer may be NULL.  All pointers are device pointers; the

@@ -383,6 +383,24 @@ extern "C" long long ptc_pool_order(int cw, int ch, int chunks, int one_wave, un
     return n;
 }
 
+// Band-major order (pool_order.h band_item, TEST TOOL): out[p] = the item at queue position p of a banded
+// launch; band[p] = band_of_tile of that item's tile; counts[b] = band_items(b)
+extern "C" long long ptc_band_order(int cw, int ch, int chunks, int bands, unsigned* out, int* band, unsigned* counts) {
+    ImageParams im{};
+    im.cw = cw;
+    im.ch = ch;
+    im.bands = bands;
+    im.band_chunks = chunks;
+    const int tiles = ((cw + 7) / 8) * ((ch + 7) / 8);
+    const unsigned n = (unsigned)tiles * (unsigned)chunks;
+    for (unsigned p = 0; p < n; ++p) {
+        out[p] = item_at(im, p, tiles);
+        band[p] = band_of_tile(im, (int)(out[p] % (unsigned)tiles));
+    }
+    for (int b = 0; b < bands; ++b) counts[b] = band_items(im, b);
+    return n;
+}
+
 // chunk_range (pool_order.h, TEST TOOL): (batch, chunk, first sample, end sample) of launch chunk gci
 extern "C" void ptc_chunk_range(int s_begin, int s_end, int batch_samples, int batch_chunks, int gci, int chunk, int* out) {
     ImageParams im{};

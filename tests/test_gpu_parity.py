@@ -519,6 +519,54 @@ def test_trace_device_two_streams_then_render(gpu, precision):
     assert np.array_equal(full, ref_full)
 
 
+@pytest.mark.parametrize("scene,w,h,spp,crop,bands", [
+    ("rtow.json", 640, 360, 24, None, 8),           # the grid's LDS pool kernel, several chunks
+    ("rtow.json", 200, 120, 3, (10, 20, 150, 90), 64),   # one chunk; more bands asked than tile rows
+    ("mesh50k", 640, 360, 12, (100, 50, 300, 200), 5),   # the one-wave kernel (triangle tree)
+    ("cornell.json", 256, 256, 16, None, 3),        # brute force
+])
+def test_trace_device_bands_bit_identical(gpu, scene, w, h, spp, crop, bands):
+    """rt_trace_device_bands (the band-by-band multi-GPU reduce): the same sums as
+    rt_trace_device bit for bit (band-major items, the same chunks and partials), every band delivered
+    once, in order, as contiguous rows covering the crop, and the callback's rows already final when it
+    runs (a copy enqueued on the stream from inside the callback equals the final rows)."""
+    import torch
+    rt = GpuRayTracer(w, h, seed=4)
+    assert rt.load_from_json(load_scene_json(scene))
+    rt.update_render_settings({"samples": spp, "maxBounces": 5})
+    lib = capi.load_library()
+    sc = rt.scene_handle()
+    st = rt.settings(crop=crop)
+    cw, ch = (crop[2], crop[3]) if crop else (w, h)
+    ref = torch.zeros(3 * cw * ch, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    capi.check(lib.rt_trace_device(sc, C.byref(st), C.c_void_p(ref.data_ptr()), None, 1, None))
+    got = torch.zeros_like(ref)
+    snap = torch.full_like(ref, float("nan"))
+    stream = torch.cuda.current_stream()
+    seen = []
+
+    def ready(b, row0, rows, user):
+        seen.append((b, row0, rows))
+        sl = slice(3 * row0 * cw, 3 * (row0 + rows) * cw)
+        snap[sl].copy_(got[sl])          # enqueued on the current stream right behind the band's reduce
+        return 0
+    cb = capi.BAND_FN(ready)
+    torch.cuda.synchronize()
+    stats = capi.Stats()
+    capi.check(lib.rt_trace_device_bands(sc, C.byref(st), C.c_void_p(got.data_ptr()), C.c_void_p(stream.cuda_stream),
+                                         bands, cb, None, C.byref(stats)))
+    torch.cuda.synchronize()
+    nb = min(bands, (ch + 7) // 8)
+    assert [b for b, _, _ in seen] == list(range(nb))
+    assert seen[0][1] == 0 and sum(r for _, _, r in seen) == ch
+    assert all(seen[k][1] + seen[k][2] == seen[k + 1][1] for k in range(nb - 1))
+    assert torch.equal(got, ref)
+    assert torch.equal(snap, ref)        # every band was final when its callback ran
+    assert stats.samples == cw * ch * spp and stats.kernel_ms > 0
+    rt.close()
+
+
 def test_sharded_step_matches_render(gpu):
     """bench.py's device path (ShardedRender.step: d_sum zeroed on torch's stream, rt_trace_device,
     rt_finalize_device, no synchronization in between) gives the host API's image frame after frame:
@@ -734,7 +782,10 @@ def tracer(w, h, spp, seed):
     rt.update_render_settings({"maxBounces": 5, "samples": spp})
     return rt
 lib = capi.load_library()
-big, small = tracer(3840, 2160, 512, 7), tracer(32, 32, 2, 9)
+# the long render: 64 one-tile items of 20000 samples each (RT_POOL_CHUNK=20000 in this process), so its
+# LDS launch holds its queue pair for a long time on only 16 workgroups, and the small launches run and
+# complete beside it: the queue pairs are handed out again and again while it holds its own
+big, small = tracer(64, 64, 20000, 7), tracer(32, 32, 2, 9)
 assert lib.rt_scene_walk(small.scene_handle(), capi.RT_PREC_F64, 0) == 2      # the grid: LDS pool launches
 ref_big = big.render(want=("mean",))["mean"]
 n, N = 32 * 32, int(sys.argv[3])
@@ -770,22 +821,21 @@ np.savez(sys.argv[2], big_equal=np.array_equal(box["big"], ref_big), bad=bad, du
 
 def test_lds_queues_owned_under_concurrent_launches(gpu, tmp_path):
     """every LDS pool launch holds a work queue of its own (queue_slots.h).  One long
-    render (RTOW 4K x 512 spp, one LDS launch) runs on one thread while another enqueues 2048 small
-    LDS-pool launches of another scene (rt_trace_device, asynchronous, on a side stream) — twice the
-    1024 queue pairs, so round 5's ring handed the long launch's pair to a small one.  Both the long
-    render and every small one are bit-identical to their solo renders."""
+    render (one LDS launch of 16 workgroups that runs for a fraction of a second) on one thread, while
+    another thread enqueues 2048 small LDS-pool launches of another scene (rt_trace_device, asynchronous,
+    on a side stream), which run and complete beside it — twice the 1024 queue pairs, so round 5's ring
+    handed the long launch's pair to a small one (whose waves then found its counter past their items).
+    Both the long render and every small one are bit-identical to their solo renders."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     p = subprocess.run([sys.executable, "-c", _QUEUES_SCRIPT, root, str(tmp_path / "q.npz"), "2048"],
-                       capture_output=True, text=True, timeout=300)
+                       capture_output=True, text=True, timeout=300, env=dict(os.environ, RT_POOL_CHUNK="20000"))
     assert p.returncode == 0, p.stderr[-2000:]
     print(p.stderr[-400:])
     r = np.load(tmp_path / "q.npz")
-    # the pairs were (nearly) all held while it ran: with ownership the 1024th acquisition waits for the
-    # long launch's pair; round 5's ring had handed it out instead
-    assert int(r["during"]) >= 1000
+    assert int(r["during"]) > 1024          # the pairs went round more than once while it ran
     assert int(r["bad"]) == 0
     assert bool(r["big_equal"])
 
@@ -893,6 +943,7 @@ def test_bench_multi_rank_rehearsal(gpu, tmp_path, world, launch):
         assert pg["batches"] == 16 and pg["value"] > 0 and pg["progress_calls_per_step"] == 15, pg
     else:
         assert line["mp_mode"]["mode"] == "ranks" and line["mp_mode"]["world_size"] == world
+        assert line["mp_mode"]["reduce_bands"] == 8       # several ranks: the band-by-band reduce (default)
     a, b = np.load(tmp_path / "n1.npz"), np.load(tmp_path / "nw.npz")
     assert int(a["samples"]) == int(b["samples"]) == 64
     assert np.allclose(a["sum"], b["sum"], rtol=SUM_RTOL, atol=1e-300)
@@ -923,16 +974,18 @@ def test_bench_rccl_world_size_1(gpu, tmp_path):
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
-           "127.0.0.1", "--master-port", str(port), bench, "--gpus", "1", "--dist-backend", "nccl", *common,
-           "--dump", str(tmp_path / "r1.npz")]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
-    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-    assert line["mp_mode"]["mode"] == "ranks" and line["mp_mode"]["world_size"] == 1
-    assert line["mp_mode"]["backend"] == "nccl" and line["n_gpus"] == 1 and line["value"] > 0
-    a, b = np.load(tmp_path / "n1.npz"), np.load(tmp_path / "r1.npz")
-    assert np.array_equal(a["sum"], b["sum"]) and np.array_equal(a["rgba8"], b["rgba8"])
+    for bands in (0, 8):        # 8: the N > 1 default, every band reduced through RCCL as it completes
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+               "127.0.0.1", "--master-port", str(port + bands), bench, "--gpus", "1", "--dist-backend", "nccl",
+               *common, "--bands", str(bands), "--dump", str(tmp_path / "r1.npz")]
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+        assert line["mp_mode"]["mode"] == "ranks" and line["mp_mode"]["world_size"] == 1
+        assert line["mp_mode"]["reduce_bands"] == bands
+        assert line["mp_mode"]["backend"] == "nccl" and line["n_gpus"] == 1 and line["value"] > 0
+        a, b = np.load(tmp_path / "n1.npz"), np.load(tmp_path / "r1.npz")
+        assert np.array_equal(a["sum"], b["sum"]) and np.array_equal(a["rgba8"], b["rgba8"]), bands
 
 
 def test_multi_device_distinct_gpus(gpu):

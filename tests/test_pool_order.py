@@ -119,3 +119,32 @@ def test_multi_device_fused_chunks_are_the_batches_chunks(s0, s1, batch, chunk, 
                 assert se <= sb
     assert sorted(seen) == list(range(s0, s1))
 
+
+
+@pytest.mark.parametrize("cw,ch,chunks,bands", [(1920, 1080, 4, 8), (1920, 1080, 1, 64), (13, 7, 3, 1), (515, 517, 5, 7),
+                                                (64, 72, 2, 9), (8, 8, 1, 1), (100, 33, 3, 5)])
+def test_band_order(cw, ch, chunks, bands):
+    """rt_trace_device_bands' item order (pool_order.h band_item): a permutation of the items in which every
+    band's items — whole tile rows, all chunks — form one contiguous run of positions, in band order, of
+    exactly band_items(b) items; the bands tile the crop's rows (the kernel counts each item into
+    band_of_tile of its tile, so every band's flag is raised by its own items only)."""
+    import ctypes as C
+    L = hc.lib()
+    L.ptc_band_order.argtypes = [C.c_int] * 4 + [C.POINTER(C.c_uint32), C.POINTER(C.c_int), C.POINTER(C.c_uint32)]
+    L.ptc_band_order.restype = C.c_longlong
+    tiles_x, tiles_y = (cw + 7) // 8, (ch + 7) // 8
+    tiles = tiles_x * tiles_y
+    out = np.zeros(tiles * chunks, dtype=np.uint32)
+    band = np.zeros(tiles * chunks, dtype=np.int32)
+    counts = np.zeros(bands, dtype=np.uint32)
+    assert L.ptc_band_order(cw, ch, chunks, bands, out.ctypes.data_as(C.POINTER(C.c_uint32)),
+                            band.ctypes.data_as(C.POINTER(C.c_int)), counts.ctypes.data_as(C.POINTER(C.c_uint32))) == out.size
+    _check(out, tiles, chunks)
+    assert np.all(np.diff(band) >= 0), "bands not contiguous / in order"
+    assert int(counts.sum()) == out.size
+    assert np.array_equal(np.bincount(band, minlength=bands), counts)
+    rows = (out % tiles) // tiles_x
+    for b in range(bands):                    # band b: tile rows [b T / B, (b + 1) T / B)
+        sel = rows[band == b]
+        if sel.size:
+            assert sel.min() == b * tiles_y // bands and sel.max() == (b + 1) * tiles_y // bands - 1
