@@ -81,9 +81,10 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks on fewer GPUs (rank -> device LOCAL_RANK %% device count, sums "
                          "reduced through host memory); never a measurement")
-    ap.add_argument("--bands", type=int, default=None,
-                    help="ranks mode: reduce the sums band by band while the later bands trace "
-                         "(rt_trace_device_bands); default 8 when several ranks reduce, else 0")
+    ap.add_argument("--bands", type=int, default=0,
+                    help="ranks mode: reduce the sums band by band as the bands complete (rt_trace_device_bands); "
+                         "0 (default): one reduce after the trace (DESIGN.md §6: the one-GPU rehearsal measured the "
+                         "banded trace 1.1 %% slower, and the RCCL kernels cannot run beside the persistent trace waves)")
     ap.add_argument("--dump", help="rank 0 writes the frame's float64 sums and RGBA8 here (.npz) after the timed steps")
     return ap.parse_args()
 
@@ -404,8 +405,7 @@ def main():
         from blenderraytracer_amd.distributed import InProcessRender
         job = InProcessRender(rt, inproc_devices)
     else:
-        bands = args.bands if args.bands is not None else (8 if world > 1 else 0)
-        job = ShardedRender(rt, rank=rank, world=world, device=torch.device("cuda", local), bands=bands)
+        job = ShardedRender(rt, rank=rank, world=world, device=torch.device("cuda", local), bands=args.bands)
     for _ in range(args.warmup):
         job.step()
     torch.cuda.synchronize()

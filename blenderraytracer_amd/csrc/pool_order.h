@@ -82,13 +82,11 @@ RT_HD unsigned band_item(const ImageParams& im, unsigned p, int tiles) {
     }
     return p;   // positions beyond the items (not taken)
 }
-// band of tile `tile` and the items that complete it
+// band of tile `tile` and the items that complete it: the largest b with floor(b T / B) <= row, i.e.
+// b T < (row + 1) B, so b = floor(((row + 1) B - 1) / T)
 RT_HD int band_of_tile(const ImageParams& im, int tile) {
     const int row = tile / ((im.cw + 7) / 8);
-    int b = (int)((long long)row * im.bands / ((im.ch + 7) / 8));
-    while (b > 0 && band_row0(im, b) > row) --b;            // floor division's neighbours
-    while (b + 1 < im.bands && band_row0(im, b + 1) <= row) ++b;
-    return b;
+    return (int)(((long long)(row + 1) * im.bands - 1) / ((im.ch + 7) / 8));
 }
 RT_HD uint32_t band_items(const ImageParams& im, int b) {
     return (uint32_t)((band_row0(im, b + 1) - band_row0(im, b)) * ((im.cw + 7) / 8)) * (uint32_t)im.band_chunks;

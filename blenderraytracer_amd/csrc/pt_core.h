@@ -1108,11 +1108,13 @@ RT_HD void copy_grid_lds(const SceneView<R>& sc, rt_u4* grec, int* gcell, int t,
 }
 
 // LDSG: the cell offsets and records come from their LDS copy in stk (ACC_GRID_LDS)
-template <class R, bool LDSG = false>
+// LEAN (ACC_GRID_LDS_LEAN): a scene without planes and boxes (scene_lean, pt_trace.hip): their loop is
+// left out of the kernel
+template <class R, bool LDSG = false, bool LEAN = false>
 RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, const BvhStack& stk) {
     const R tmin = (R)0.001;
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
-    brute_planes_boxes(sc, o, d, tmin, b);
+    if constexpr (!LEAN) brute_planes_boxes(sc, o, d, tmin, b);
     float tl = bvh_tlimit(b.t);
     const R a = dot(d, d), ya = root_rcp(a);
     FilterRay fr{};
@@ -1190,7 +1192,12 @@ RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work
 // ACC_BVH_TRI_LDS: the general ordered walk (scenes with triangles) with the triangle tree's top levels in
 // LDS (trace_pool_lds_kernel's persistent multi-wave workgroups, round 6)
 enum Accel : int { ACC_BRUTE = 0, ACC_BVH = 2, ACC_BVH_STACK = 3, ACC_BVH_SPHERES = 4, ACC_BVH_SPHERES_LDS = 5,
-                   ACC_GRID = 6, ACC_GRID_LDS = 7, ACC_BVH_TRI_LDS = 8 };
+                   ACC_GRID = 6, ACC_GRID_LDS = 7, ACC_BVH_TRI_LDS = 8, ACC_GRID_LDS_LEAN = 9 };
+// ACC_GRID_LDS_LEAN: ACC_GRID_LDS compiled for the common scene shape only — spheres alone (no planes,
+// boxes or triangles), the sky gradient, the perspective camera, supersampling AA (scene_lean,
+// pt_trace.hip): the other branches and the scene constants they read leave the kernel, so fewer scalars
+// stay live across the segment loop (SGPR spills)
+template <int ACC> constexpr bool lean_acc() { return ACC == ACC_GRID_LDS_LEAN; }
 
 template <class R, int ACC>
 RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
@@ -1200,6 +1207,7 @@ RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
     else if constexpr (ACC == ACC_BVH_SPHERES_LDS) return closest_hit_bvh<R, true, false, true>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_GRID) return closest_hit_grid<R>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_GRID_LDS) return closest_hit_grid<R, true>(sc, o, d, w, stk);
+    else if constexpr (ACC == ACC_GRID_LDS_LEAN) return closest_hit_grid<R, true, true>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_BVH_TRI_LDS) return closest_hit_bvh<R, true, true, false, true>(sc, o, d, w, stk);
     else return closest_hit<R>(sc, o, d);
 }
@@ -1213,13 +1221,14 @@ RT_HD void set_face(Hit<R>& h, V3<R> d, V3<R> outward) {       // math.js:55-58
     h.n = h.front ? outward : outward * (R)-1;
 }
 
-// Rebuild the HitRecord of the winning primitive (point = origin + dir*t, math.js:41).
-template <class R>
+// Rebuild the HitRecord of the winning primitive (point = origin + dir*t, math.js:41).  LEAN: a sphere
+// (the only primitive a lean scene has)
+template <class R, bool LEAN = false>
 RT_HD Hit<R> hit_record(const SceneView<R>& sc, V3<R> o, V3<R> d, const Closest<R>& c) {
     Hit<R> h;
     h.p = o + d * c.t;
     h.mat = c.mat;
-    if (c.kind == HIT_SPHERE) {
+    if (LEAN || c.kind == HIT_SPHERE) {
         const SphereRec<R> s = sc.spheres[c.idx];
 #if RT_DIV_RCP
         set_face(h, d, vdiv_rcp(h.p - mk(s.cx, s.cy, s.cz), sc.sphere_r[c.idx], sc.sphere_inv_r[c.idx]));
@@ -1335,9 +1344,13 @@ __host__ __device__ RT_COLD V3<R> background_procedural(const SceneView<R>& sc, 
 }
 
 // unit: normalize(d), computed by the caller (shade_segment shares it with the scatter of other lanes)
-template <class R>
+template <class R, bool LEAN = false>
 __host__ __device__ V3<R> background(const SceneView<R>& sc, V3<R> d, V3<R> unit) {
     const R I = sc.sky_intensity;
+    if constexpr (LEAN) {                                                             // skyGradient only
+        R t = (R)0.5 * (unit.y + (R)1);
+        return (mk<R>(1, 1, 1) * ((R)1 - t) + mk<R>(0.5, 0.7, 1.0) * t) * I;
+    }
     switch (sc.background) {
     case 0: {                                                                         // skyGradient
         R t = (R)0.5 * (unit.y + (R)1);

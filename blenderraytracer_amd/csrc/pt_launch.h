@@ -162,6 +162,10 @@ struct GammaTable {
 hipError_t launch_finalize(const FinalizeParams& p, const double* sum, double* mean, float* post, uint8_t* rgba8,
                            hipStream_t stream, const GammaTable* thresholds = nullptr);
 bool preview_thresholds_ok(double gamma);
+// launch_reduce of a progressive batch and its running frame (preview_kernel's bytes through `table`, into
+// rgba8) in one kernel: reduce_preview_kernel (pt_trace.hip).  When the gate skips the batch, neither runs
+hipError_t launch_reduce_preview(const ImageParams& im, double* sum, const double* part, bool tri_bvh, hipStream_t stream,
+                                 const ReduceGate* gate, const FinalizeParams& fp, const GammaTable* table, uint8_t* rgba8);
 hipError_t launch_gamma_thresholds(double gamma, GammaTable* T, hipStream_t stream);
 hipError_t launch_denoise(int w, int h, double w1, double w2, const float* in, float* out, uint8_t* rgba8,
                           hipStream_t stream);

@@ -86,7 +86,8 @@ constexpr bool uses_stack() {
 
 template <class R, int ACC>
 constexpr int waves_per_simd() {
-    if constexpr (ACC == ACC_GRID || ACC == ACC_GRID_LDS) return sizeof(R) == 8 ? RT_GRID_WAVES_PER_SIMD : RT_GRID_WAVES_F32;
+    if constexpr (ACC == ACC_GRID || ACC == ACC_GRID_LDS || ACC == ACC_GRID_LDS_LEAN)
+        return sizeof(R) == 8 ? RT_GRID_WAVES_PER_SIMD : RT_GRID_WAVES_F32;
     if constexpr (ACC == ACC_BVH_SPHERES) return sizeof(R) == 8 ? RT_SPHERES_WAVES_PER_SIMD : RT_SPHERES_WAVES_F32;
     if constexpr (ACC == ACC_BVH_SPHERES_LDS) return sizeof(R) == 8 ? RT_LDS_OCC_F64 : RT_LDS_OCC_F32;
     if constexpr (ACC == ACC_BVH_TRI_LDS) return sizeof(R) == 8 ? RT_BVH_WAVES_PER_SIMD : RT_BVH_WAVES_F32;
@@ -464,7 +465,7 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
         T = mk<R>(1, 1, 1);
         depth = im.max_depth;
         isegs = 0;
-        start_sample<R, sizeof(R) == 4>(sc, im, i, j, pkey, s, g, o, d);
+        start_sample<R, sizeof(R) == 4, lean_acc<ACC>()>(sc, im, i, j, pkey, s, g, o, d);
     };
     uint32_t next = 64;                       // items [0, 64) are dealt to lanes 0..63 up front
     bool live = (uint32_t)lane < total;
@@ -479,7 +480,7 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
             ++res.segments;
             ++isegs;
             V3<R> L;
-            waiting = shade_segment(sc, c, o, d, T, depth, g, L, lmats);
+            waiting = shade_segment<R, lean_acc<ACC>()>(sc, c, o, d, T, depth, g, L, lmats);
             if (RT_PROFILE) res.cyc[1] += RT_TICK() - t1;
             if (waiting) {
                 if (COUNT) {
@@ -580,7 +581,7 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
 #endif
 template <class R, int ACC = ACC_BVH_SPHERES_LDS>
 constexpr int lds_waves() {
-    if constexpr (ACC == ACC_GRID_LDS) return sizeof(R) == 8 ? RT_GRID_LDS_WAVES_F64 : RT_GRID_LDS_WAVES_F32;
+    if constexpr (ACC == ACC_GRID_LDS || ACC == ACC_GRID_LDS_LEAN) return sizeof(R) == 8 ? RT_GRID_LDS_WAVES_F64 : RT_GRID_LDS_WAVES_F32;
     if constexpr (ACC == ACC_BVH_TRI_LDS) return sizeof(R) == 8 ? RT_TRI_LDS_WAVES_F64 : RT_TRI_LDS_WAVES_F32;
     return sizeof(R) == 8 ? RT_LDS_WAVES_F64 : RT_LDS_WAVES_F32;
 }
@@ -614,7 +615,7 @@ void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, c
     __shared__ double acc_all[W * 3 * 64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     BvhStack stk{nullptr, 0};
-    if constexpr (ACC == ACC_GRID_LDS) {
+    if constexpr (ACC == ACC_GRID_LDS || ACC == ACC_GRID_LDS_LEAN) {
         rt_u4* grec = reinterpret_cast<rt_u4*>(lds_dyn);
         int* gcell = reinterpret_cast<int*>(lds_dyn + grid_lds_rec_bytes(sc));
         copy_grid_lds(sc, grec, gcell, threadIdx.x, 64 * W);
@@ -645,7 +646,7 @@ void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, c
     acc[128 + lane] = 0;
     const MatRec<R>* lmats = nullptr;
 #if RT_MAT_LDS
-    if constexpr (ACC == ACC_GRID_LDS) {      // A/B: the material records after the grid's copy
+    if constexpr (ACC == ACC_GRID_LDS || ACC == ACC_GRID_LDS_LEAN) {   // A/B: the material records after the grid's copy
         MatRec<R>* mm = reinterpret_cast<MatRec<R>*>(lds_dyn + ((grid_lds_bytes(sc) + 15) & ~(size_t)15));
         for (int k = threadIdx.x; k < sc.num_mats; k += 64 * W) mm[k] = sc.mats[k];
         lmats = mm;
@@ -1116,6 +1117,15 @@ void forget_pool_launches(const uint32_t* cancel) {
 void register_cancel_word(const uint32_t* cancel, int device, uint32_t* word, uint32_t gen) {
     std::lock_guard<std::mutex> g(g_launch_mu);
     g_words.push_back(CancelWord{cancel, device, word, gen});
+    // the device's cancel stream now, not in the first cancel (its creation took ~7 ms there)
+    if (!g_cancel_stream[device & 63]) {
+        int cur = 0;
+        hipStream_t cs = nullptr;
+        if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(device) == hipSuccess) {
+            (void)cancel_stream(device, &cs);
+            (void)hipSetDevice(cur);
+        }
+    }
 }
 
 static int device_cus() {
@@ -1130,37 +1140,60 @@ static int device_cus() {
     return n;
 }
 
+// one trace_pool_lds_kernel launch with its own work queue (lb: its dynamic LDS)
+template <class R, int LACC>
+static hipError_t launch_lds_pool(const TraceArgs<R>& a, bool count, double* part, int tiles, int chunks, int chunk,
+                                  size_t lb, hipStream_t stream) {
+    int dev = 0, qi = 0;
+    if (const hipError_t e = acquire_queue(&dev, &qi)) return e;
+    const long long items = (long long)tiles * chunks;
+    constexpr int W = lds_waves<R, LACC>();
+    const int resident = device_cus() * 4 * waves_per_simd<R, LACC>() / W;
+    const int grid = (int)std::min<long long>(resident, (items + W - 1) / W);
+    if (count) hipLaunchKernelGGL((trace_pool_lds_kernel<R, true, LACC>), dim3(grid), dim3(64 * W), lb, stream,
+                                  a, part, tiles, chunk, (int)items, qi);
+    else hipLaunchKernelGGL((trace_pool_lds_kernel<R, false, LACC>), dim3(grid), dim3(64 * W), lb, stream,
+                            a, part, tiles, chunk, (int)items, qi);
+    const hipError_t e = hipGetLastError();
+    const hipError_t eh = hold_queue(dev, qi, stream, e == hipSuccess);
+    if (e != hipSuccess) return e;
+    if (eh != hipSuccess) return eh;
+    if (!a.c.cancel) return hipSuccess;
+    return register_pool_launch(a.c, dev, qi, (uint32_t)items, stream);
+}
+
+// The lean grid kernel (ACC_GRID_LDS_LEAN) serves this launch: spheres only (a grid scene), no planes or
+// boxes, the sky gradient, the perspective camera, supersampling AA.  RT_LEAN=0: never (A/B)
+#ifndef RT_LEAN
+#define RT_LEAN 1
+#endif
+template <class R>
+static bool scene_lean(const SceneView<R>& sc, const ImageParams& im) {
+    static const int v = [] {
+        const char* e = getenv("RT_LEAN");
+        return e ? atoi(e) : RT_LEAN;
+    }();
+    return v != 0 && sc.num_planes == 0 && sc.num_boxes == 0 && sc.num_tri_nodes == 0 && sc.background == 0 &&
+           !sc.cam_ortho && im.aa_mode == 0;
+}
+
 template <class R, int ACC>
 static hipError_t launch_pool_kernel(const TraceArgs<R>& a0, bool count, double* part, int tiles, int chunks,
                                      int chunk, hipStream_t stream) {
-    if constexpr (ACC == ACC_BVH_SPHERES || ACC == ACC_GRID || ACC == ACC_BVH_STACK) {
-        constexpr int LACC = ACC == ACC_GRID ? ACC_GRID_LDS : ACC == ACC_BVH_STACK ? ACC_BVH_TRI_LDS : ACC_BVH_SPHERES_LDS;
+    if constexpr (ACC == ACC_GRID) {
+        if (const size_t lb = lds_grid_bytes(a0.sc)) {
+            if (scene_lean(a0.sc, a0.im)) return launch_lds_pool<R, ACC_GRID_LDS_LEAN>(a0, count, part, tiles, chunks, chunk, lb, stream);
+            return launch_lds_pool<R, ACC_GRID_LDS>(a0, count, part, tiles, chunks, chunk, lb, stream);
+        }
+    } else if constexpr (ACC == ACC_BVH_SPHERES) {
+        if (const size_t lb = lds_nodes_bytes(a0.sc))
+            return launch_lds_pool<R, ACC_BVH_SPHERES_LDS>(a0, count, part, tiles, chunks, chunk, lb, stream);
+    } else if constexpr (ACC == ACC_BVH_STACK) {
         TraceArgs<R> a = a0;
-        size_t lb = 0;
-        if constexpr (ACC == ACC_BVH_STACK) {
-            a.sc.tri_lds_nodes = lds_tri_nodes(a.sc);
-            lb = a.sc.tri_lds_nodes ? lds_tri_bytes(a.sc, a.sc.tri_lds_nodes) : 0;
-        } else {
-            lb = ACC == ACC_GRID ? lds_grid_bytes(a.sc) : lds_nodes_bytes(a.sc);
-        }
-        if (lb) {
-            int dev = 0, qi = 0;
-            if (const hipError_t e = acquire_queue(&dev, &qi)) return e;
-            const long long items = (long long)tiles * chunks;
-            constexpr int W = lds_waves<R, LACC>();
-            const int resident = device_cus() * 4 * waves_per_simd<R, LACC>() / W;
-            const int grid = (int)std::min<long long>(resident, (items + W - 1) / W);
-            if (count) hipLaunchKernelGGL((trace_pool_lds_kernel<R, true, LACC>), dim3(grid), dim3(64 * W), lb, stream,
-                                          a, part, tiles, chunk, (int)items, qi);
-            else hipLaunchKernelGGL((trace_pool_lds_kernel<R, false, LACC>), dim3(grid), dim3(64 * W), lb, stream,
-                                    a, part, tiles, chunk, (int)items, qi);
-            const hipError_t e = hipGetLastError();
-            const hipError_t eh = hold_queue(dev, qi, stream, e == hipSuccess);
-            if (e != hipSuccess) return e;
-            if (eh != hipSuccess) return eh;
-            if (!a.c.cancel) return hipSuccess;
-            return register_pool_launch(a.c, dev, qi, (uint32_t)items, stream);
-        }
+        a.sc.tri_lds_nodes = lds_tri_nodes(a.sc);
+        if (a.sc.tri_lds_nodes)
+            return launch_lds_pool<R, ACC_BVH_TRI_LDS>(a, count, part, tiles, chunks, chunk,
+                                                       lds_tri_bytes(a.sc, a.sc.tri_lds_nodes), stream);
     }
     return launch_onewave_pool<R, ACC>(a0, count, part, tiles, chunks, chunk, stream);
 }
@@ -1612,6 +1645,58 @@ __global__ __launch_bounds__(64) void preview_kernel(const FinalizeParams p, con
         o |= b << (8 * k);
     }
     *reinterpret_cast<uint32_t*>(rgba8 + 4 * q) = o;
+}
+
+// A progressive batch's reduce and its running frame in one pass (RT_FUSED_PREVIEW): each thread adds its
+// pixel's chunk partials to the sums exactly as reduce_kernel does, then computes the pixel's RGBA8 byte
+// from the new sums exactly as preview_kernel does (the same binary64 values: identical bytes).  One
+// one-wave workgroup per tile instead of two kernels' (the trace's one-wave workgroups of triangle scenes
+// leave no VGPRs beside them, so every side workgroup takes a trace wave's slot), and the sums are not
+// read a second time.  At most 32 VGPRs (16 waves/SIMD), like the two kernels it replaces.
+__global__ __launch_bounds__(64, 16) void reduce_preview_kernel(const ImageParams im, double* __restrict__ sum,
+                                                                const double* __restrict__ part, const int tiles,
+                                                                const int chunks, const uint32_t* __restrict__ skip,
+                                                                const FinalizeParams p, const GammaTable* __restrict__ g,
+                                                                uint8_t* __restrict__ rgba8) {
+    const int tile = blockIdx.x, m = threadIdx.x;
+    if (tile >= tiles || (skip && *skip)) return;
+    const Tile t = tile_of(im, tile);
+    if (m >= t.nv) return;
+    const size_t q = (size_t)(t.y0 + m / t.vw) * im.cw + (t.x0 + m % t.vw);
+    double a[3] = {sum[3 * q], sum[3 * q + 1], sum[3 * q + 2]};
+    const double* pp = part + (size_t)tile * 3 * 64 + m;
+    const size_t stride = (size_t)tiles * 3 * 64;
+    for (int c = 0; c < chunks; ++c, pp += stride) {
+        a[0] += pp[0];
+        a[1] += pp[64];
+        a[2] += pp[128];
+    }
+    sum[3 * q] = a[0]; sum[3 * q + 1] = a[1]; sum[3 * q + 2] = a[2];
+    const uint32_t ne = min(g->n_exc, (uint32_t)kGammaExc);
+    uint32_t o = 255u << 24;
+#pragma unroll 1
+    for (int k = 0; k < 3; ++k) {
+        const double x = a[k] / (double)p.samples * p.exposure;
+        double tm;
+        if (p.tone_map == 1) tm = js_max<double>(0.0, (x * (2.51 * x + 0.03)) / (x * (2.43 * x + 0.59) + 0.14));
+        else if (p.tone_map == 2) tm = x;
+        else tm = x / (1.0 + x);
+        uint32_t b = gamma_count(g->t, tm);
+        for (uint32_t e = 0; e < ne; ++e)
+            if (g->exc_tm[e] == tm) b = g->exc_byte[e];
+        o |= b << (8 * k);
+    }
+    *reinterpret_cast<uint32_t*>(rgba8 + 4 * q) = o;
+}
+
+hipError_t launch_reduce_preview(const ImageParams& im, double* sum, const double* part, bool tri_bvh, hipStream_t stream,
+                                 const ReduceGate* gate, const FinalizeParams& fp, const GammaTable* table, uint8_t* rgba8) {
+    if (im.cw <= 0 || im.ch <= 0 || im.s_end <= im.s_begin) return hipSuccess;
+    const PoolPlan pl = pool_plan(im.cw, im.ch, im.s_end - im.s_begin, tri_bvh, im.pool_chunk);
+    if (gate) hipLaunchKernelGGL(reduce_gate_kernel, dim3(1), dim3(64), 0, stream, *gate);
+    hipLaunchKernelGGL(reduce_preview_kernel, dim3((unsigned)pl.tiles), dim3(64), 0, stream, im, sum, part, pl.tiles,
+                       pl.chunks, (const uint32_t*)(gate ? gate->skip : nullptr), fp, table, rgba8);
+    return hipGetLastError();
 }
 
 // thresholds of gamma_byte for this gamma: only for gammas in [kGammaMin, kGammaMax] (pt_launch.h), the

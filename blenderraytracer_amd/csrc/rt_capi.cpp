@@ -1199,6 +1199,21 @@ int render_impl(rt_scene* sc, const rt_settings* s_in, const rt_output* out, rt_
             gate.skip = h.gate_skip.p;
             gp = &gate;
         }
+        // fused batches with running frames: RT_FUSED_PREVIEW=1 (A/B) the batch's reduce and its frame in one
+        // kernel (reduce_preview_kernel) — measured slower: mesh50k 22 batches with running frames 77.6 vs
+        // 76.1 ms kernel time for the two kernels (config 3: 96.0 vs 95.9), DESIGN.md §4
+        static const bool fused_preview_env = getenv("RT_FUSED_PREVIEW") && getenv("RT_FUSED_PREVIEW")[0] == '1';
+        const bool fuse_prev = fused && fused_preview_env && want_preview && be < s1 && thresholds;
+        bool previewed = false;
+        auto reduce_batch = [&](const ImageParams& bi, const double* src) -> hipError_t {
+            if (!fuse_prev) return launch_reduce(bi, h.sum.p, src, sc->tri_bvh, h.stream, gp);
+            FinalizeParams fp{(int)n, be - base, s->tone_map, s->exposure, s->gamma};
+            hipError_t e = launch_reduce_preview(bi, h.sum.p, src, sc->tri_bvh, h.stream, gp, fp, thresholds->table(),
+                                                 sc->preview_dev[kb % ring]);
+            if (e == hipSuccess) e = gamma_used(thresholds, h.stream);
+            previewed = e == hipSuccess;
+            return e;
+        };
         auto with_cancel = [&](Counters c) {
             if (gated) {
                 if (item_cancel) c.cancel = sc->ctl_dev + kCtlCancel;
@@ -1261,7 +1276,7 @@ int render_impl(rt_scene* sc, const rt_settings* s_in, const rt_output* out, rt_
             if (&ds == &h) {
                 HIP_TRY(hipSetDevice(h.device));
                 if (!flagged) HIP_TRY(hipStreamWaitEvent(h.stream, h.fused_done, 0));
-                HIP_TRY(launch_reduce(bi, h.sum.p, src, sc->tri_bvh, h.stream, gp));
+                HIP_TRY(reduce_batch(bi, src));
             } else {                              // a replica's batch: its partials to the home device first
                 MergeSlot& m = sc->merge[d];
                 const int j = lb % kSlots;
@@ -1276,7 +1291,7 @@ int render_impl(rt_scene* sc, const rt_settings* s_in, const rt_output* out, rt_
                 HIP_TRY(hipEventRecord(ds.traced[j], ds.stream));
                 HIP_TRY(hipSetDevice(h.device));
                 HIP_TRY(hipStreamWaitEvent(h.stream, ds.traced[j], 0));
-                HIP_TRY(launch_reduce(bi, h.sum.p, m.stage[j].p, sc->tri_bvh, h.stream, gp));
+                HIP_TRY(reduce_batch(bi, m.stage[j].p));
                 HIP_TRY(hipEventRecord(m.stage_free[j], h.stream));
                 m.stage_used[j] = true;
             }
@@ -1305,7 +1320,7 @@ int render_impl(rt_scene* sc, const rt_settings* s_in, const rt_output* out, rt_
         int r;
         if (nsh > 1 && !whole && (r = merge_shards(sc, states, n, want_segs, want_draws))) return r;
         HIP_TRY(hipSetDevice(h.device));
-        if (want_preview && be < s1) {            // the running frame: mean over the samples so far
+        if (want_preview && be < s1 && !previewed) {   // the running frame: mean over the samples so far
             // written by the epilogue kernel straight into pinned host memory (over PCIe): a
             // hipMemcpyAsync here is a blit kernel that waits for wave slots behind the trace waves
             // (measured 7-15 ms per 8-MB frame while batches overlap)

@@ -843,10 +843,12 @@ def test_lds_queues_owned_under_concurrent_launches(gpu, tmp_path):
 def test_cancel_latency_triangle_scene(gpu, tmp_path):
     """The same in-batch cancel on config 5 (mesh50k 1920x1080 x 256 spp in four batches): its walk runs
     in the one-wave pool kernel, whose workgroups read the cancel word as their item starts (the LDS
-    kernels' queue move does not apply).  Measured 25 ms against a 114-ms frame: the items in flight
-    finish in ~1 ms, but the fused launch's remaining one-wave workgroups (~400k) still pass through the
-    dispatcher, each exiting after its read.  Asserted: rt_render returns within half a frame and the
-    checkpoint resumes bit-exactly."""
+    kernels' queue move does not apply).  Round 5: 25 ms against a 114-ms frame — the fused launch's
+    remaining one-wave workgroups (~400k) passed through the dispatcher, each reading the word over PCIe
+    and writing the host `aborted` word.  Round 6: the word is a device-memory copy set from a
+    high-priority stream (an L2 read) and skipping workgroups write nothing: 5 ms (scripts/probe_cancel.py).
+    Asserted: rt_render returns within an eighth of a frame and the checkpoint
+    resumes bit-exactly."""
     import os
     import subprocess
     import sys
@@ -859,7 +861,7 @@ def test_cancel_latency_triangle_scene(gpu, tmp_path):
     print(f"cancel-to-return {latency * 1e3:.2f} ms; frame {frame * 1e3:.1f} ms; checkpoint {done} samples; {r['rc']}")
     assert "CANCELLED" in str(r["rc"])
     assert done in (0, 64, 128, 192)
-    assert latency < frame / 2
+    assert latency < frame / 8
     assert bool(r["equal"])
 
 
@@ -928,7 +930,7 @@ def test_bench_multi_rank_rehearsal(gpu, tmp_path, world, launch):
     if launch == "torchrun":
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                "--master-addr", "127.0.0.1", "--master-port", str(29611 + world), bench, "--gpus", str(world),
-               "--dist-backend", "gloo", *common, *dump]
+               "--dist-backend", "gloo", "--bands", "8", *common, *dump]      # the band-by-band reduce
     elif launch == "spawn":
         cmd = [sys.executable, bench, "--gpus", str(world), "--dist-backend", "gloo", *common, *dump]
     else:
@@ -943,7 +945,7 @@ def test_bench_multi_rank_rehearsal(gpu, tmp_path, world, launch):
         assert pg["batches"] == 16 and pg["value"] > 0 and pg["progress_calls_per_step"] == 15, pg
     else:
         assert line["mp_mode"]["mode"] == "ranks" and line["mp_mode"]["world_size"] == world
-        assert line["mp_mode"]["reduce_bands"] == 8       # several ranks: the band-by-band reduce (default)
+        assert line["mp_mode"]["reduce_bands"] == (8 if launch == "torchrun" else 0)
     a, b = np.load(tmp_path / "n1.npz"), np.load(tmp_path / "nw.npz")
     assert int(a["samples"]) == int(b["samples"]) == 64
     assert np.allclose(a["sum"], b["sum"], rtol=SUM_RTOL, atol=1e-300)
