@@ -382,13 +382,20 @@ RT_HD bool sphere_filter_pass(const SphereFilter& s, const FilterRay& r) {
     return !(__builtin_fmaf(hb, hb, -cc) < 0.0f);
 }
 
+// Scene features a trace kernel is compiled for (FEAT template arguments; the lean kernels, pt_trace.hip
+// scene_lean): planes, boxes and triangles among the primitives, every background (else the sky gradient
+// only), the orthographic camera and the stochastic / centre AA modes (else the perspective camera with
+// supersampling).  A kernel compiled without a feature holds none of its code, nor the scene constants
+// that code reads, so fewer scalars stay live across the segment loop (SGPR spills).
+enum Feat : int { F_PLANES = 1, F_BOXES = 2, F_TRIS = 4, F_BGALL = 8, F_CAMALL = 16, F_ALL = 31 };
+
 // Closest hit over the whole world: World.hit (world.js:20-33) with every object's hit() inlined.
 // All lanes walk the same primitive list in the same order, so every record load — including the
 // material index, taken at accept time — is wave-uniform (scalar loads, no LDS).  Only
 // (t, kind, index, material) is tracked; the hit record is rebuilt afterwards from (t, primitive),
 // which is exact because no primitive's chosen t depends on tMax.
-template <class R>
-RT_HD Closest<R> closest_hit(const SceneView<R>& sc, V3<R> o, V3<R> d) {
+template <class R, int FEAT = F_ALL>
+RT_HD Closest<R> closest_hit_runs(const SceneView<R>& sc, V3<R> o, V3<R> d) {
     const R tmin = (R)0.001;
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0};
     const R a = dot(d, d);
@@ -409,7 +416,7 @@ RT_UNROLL(RT_SPHERE_UNROLL)
             }
 #pragma unroll 2
             for (int i = run.begin; i < run.end; ++i) sphere_test_f64(sc, o, d, a, tmin, i, b);
-        } else if (run.kind == RUN_PLANES) {
+        } else if ((FEAT & F_PLANES) != 0 && run.kind == RUN_PLANES) {
             for (int i = run.begin; i < run.end; ++i) {                       // geometry.js:56-74
                 const PlaneRec<R> p = sc.planes[i];
                 R denom = p.nx * d.x + p.ny * d.y + p.nz * d.z;
@@ -418,7 +425,7 @@ RT_UNROLL(RT_SPHERE_UNROLL)
                 if (t < tmin || t > b.t) continue;
                 if (t < b.t) b = Closest<R>{t, HIT_PLANE, i, sc.plane_mat[i]};
             }
-        } else if (run.kind == RUN_BOXES) {
+        } else if ((FEAT & F_BOXES) != 0 && run.kind == RUN_BOXES) {
             for (int i = run.begin; i < run.end; ++i) {                       // geometry.js:85-117
                 const BoxRec<R> bx = sc.boxes[i];
                 R t0 = (bx.mnx - o.x) / d.x, t1 = (bx.mxx - o.x) / d.x;
@@ -437,7 +444,7 @@ RT_UNROLL(RT_SPHERE_UNROLL)
                 if (t < tmin || t > b.t) continue;                            // NaN passes here ...
                 if (t < b.t) b = Closest<R>{t, HIT_BOX, i, sc.box_mat[i]};    // ... and fails here
             }
-        } else {                                                              // geometry.js:148-188, 248-262
+        } else if ((FEAT & F_TRIS) != 0) {                                    // geometry.js:148-188, 248-262
             const bool mesh = run.kind == RUN_MESH;
             R local = b.t;
             int local_idx = -1;
@@ -464,6 +471,8 @@ RT_UNROLL(RT_SPHERE_UNROLL)
     }
     return b;
 }
+template <class R>
+RT_HD Closest<R> closest_hit(const SceneView<R>& sc, V3<R> o, V3<R> d) { return closest_hit_runs<R, F_ALL>(sc, o, d); }
 
 // ---- BVH mode ---------------------------------------------------------------------------------------
 // World.hit's result is the minimum of a total order over the candidates: every object's candidate t
@@ -861,8 +870,9 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
 }
 
 // Planes and boxes (usually few, often large) brute force, with their World.objects index.
-template <class R>
+template <class R, int FEAT = F_ALL>
 RT_HD void brute_planes_boxes(const SceneView<R>& sc, V3<R> o, V3<R> d, R tmin, Closest<R>& b) {
+    if constexpr ((FEAT & F_PLANES) != 0)
     for (int i = 0; i < sc.num_planes; ++i) {                                 // geometry.js:56-74
         const PlaneRec<R> p = sc.planes[i];
         R denom = p.nx * d.x + p.ny * d.y + p.nz * d.z;
@@ -872,6 +882,7 @@ RT_HD void brute_planes_boxes(const SceneView<R>& sc, V3<R> o, V3<R> d, R tmin, 
         const int obj = sc.plane_obj[i];
         if (better(t, obj, i, b)) b = Closest<R>{t, HIT_PLANE, i, sc.plane_mat[i], obj};
     }
+    if constexpr ((FEAT & F_BOXES) != 0)
     for (int i = 0; i < sc.num_boxes; ++i) {                                  // geometry.js:85-117
         const BoxRec<R> bx = sc.boxes[i];
         R t0 = (bx.mnx - o.x) / d.x, t1 = (bx.mxx - o.x) / d.x;
@@ -972,11 +983,11 @@ RT_HD void tri_leaf_filtered(const SceneView<R>& sc, int fc, const TriRay& tr, V
 // TRI = false (ACC_BVH_SPHERES): scenes without triangles; the triangle walk's code is left out.
 // LDSN: the sphere tree's nodes are read from their LDS copy in stk (ACC_BVH_SPHERES_LDS).
 // TLDS: the triangle tree's top levels are read from their LDS copy in stk (ACC_BVH_TRI_LDS).
-template <class R, bool WIDE, bool TRI = true, bool LDSN = false, bool TLDS = false>
+template <class R, bool WIDE, bool TRI = true, bool LDSN = false, bool TLDS = false, int FEAT = F_ALL>
 RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
     const R tmin = (R)0.001;
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
-    brute_planes_boxes(sc, o, d, tmin, b);
+    brute_planes_boxes<R, FEAT>(sc, o, d, tmin, b);
     const BvhRay br = make_bvh_ray(o, d);
     float tl = bvh_tlimit(b.t);
     if (sc.num_sphere_nodes > 0 || sc.num_big_spheres > 0) {
@@ -1108,13 +1119,12 @@ RT_HD void copy_grid_lds(const SceneView<R>& sc, rt_u4* grec, int* gcell, int t,
 }
 
 // LDSG: the cell offsets and records come from their LDS copy in stk (ACC_GRID_LDS)
-// LEAN (ACC_GRID_LDS_LEAN): a scene without planes and boxes (scene_lean, pt_trace.hip): their loop is
-// left out of the kernel
-template <class R, bool LDSG = false, bool LEAN = false>
+// FEAT: the scene features compiled in (Feat; the grid's lean kernel: spheres only)
+template <class R, bool LDSG = false, int FEAT = F_ALL>
 RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, const BvhStack& stk) {
     const R tmin = (R)0.001;
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
-    if constexpr (!LEAN) brute_planes_boxes(sc, o, d, tmin, b);
+    brute_planes_boxes<R, FEAT>(sc, o, d, tmin, b);
     float tl = bvh_tlimit(b.t);
     const R a = dot(d, d), ya = root_rcp(a);
     FilterRay fr{};
@@ -1191,13 +1201,18 @@ RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work
 // ACC_GRID_LDS: the same walk with the grid's cell offsets and records (binary64: their filters) in LDS
 // ACC_BVH_TRI_LDS: the general ordered walk (scenes with triangles) with the triangle tree's top levels in
 // LDS (trace_pool_lds_kernel's persistent multi-wave workgroups, round 6)
-enum Accel : int { ACC_BRUTE = 0, ACC_BVH = 2, ACC_BVH_STACK = 3, ACC_BVH_SPHERES = 4, ACC_BVH_SPHERES_LDS = 5,
-                   ACC_GRID = 6, ACC_GRID_LDS = 7, ACC_BVH_TRI_LDS = 8, ACC_GRID_LDS_LEAN = 9 };
-// ACC_GRID_LDS_LEAN: ACC_GRID_LDS compiled for the common scene shape only — spheres alone (no planes,
-// boxes or triangles), the sky gradient, the perspective camera, supersampling AA (scene_lean,
-// pt_trace.hip): the other branches and the scene constants they read leave the kernel, so fewer scalars
-// stay live across the segment loop (SGPR spills)
-template <int ACC> constexpr bool lean_acc() { return ACC == ACC_GRID_LDS_LEAN; }
+enum Accel : int { ACC_BRUTE = 0, ACC_BRUTE_LEAN = 1, ACC_BVH = 2, ACC_BVH_STACK = 3, ACC_BVH_SPHERES = 4, ACC_BVH_SPHERES_LDS = 5,
+                   ACC_GRID = 6, ACC_GRID_LDS = 7, ACC_BVH_TRI_LDS = 8, ACC_GRID_LDS_LEAN = 9,
+                   ACC_BVH_STACK_LEAN = 10 };
+// The lean kernels (pt_trace.hip scene_feat): compiled for the common scene shapes only, the sky
+// gradient, the perspective camera and supersampling AA —
+//   ACC_GRID_LDS_LEAN: ACC_GRID_LDS for spheres alone (no planes, boxes or triangles; RTOW);
+//   ACC_BVH_STACK_LEAN: ACC_BVH_STACK without boxes (spheres, planes, triangles; config 5)
+//   ACC_BRUTE_LEAN: World order for spheres and planes (config 2's Cornell box)
+template <int ACC> constexpr int feat_of() {
+    return ACC == ACC_GRID_LDS_LEAN ? 0 : ACC == ACC_BVH_STACK_LEAN ? (F_PLANES | F_TRIS)
+         : ACC == ACC_BRUTE_LEAN ? F_PLANES : F_ALL;
+}
 
 template <class R, int ACC>
 RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
@@ -1207,9 +1222,11 @@ RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
     else if constexpr (ACC == ACC_BVH_SPHERES_LDS) return closest_hit_bvh<R, true, false, true>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_GRID) return closest_hit_grid<R>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_GRID_LDS) return closest_hit_grid<R, true>(sc, o, d, w, stk);
-    else if constexpr (ACC == ACC_GRID_LDS_LEAN) return closest_hit_grid<R, true, true>(sc, o, d, w, stk);
+    else if constexpr (ACC == ACC_GRID_LDS_LEAN) return closest_hit_grid<R, true, feat_of<ACC>()>(sc, o, d, w, stk);
+    else if constexpr (ACC == ACC_BVH_STACK_LEAN)
+        return closest_hit_bvh<R, true, true, false, false, feat_of<ACC>()>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_BVH_TRI_LDS) return closest_hit_bvh<R, true, true, false, true>(sc, o, d, w, stk);
-    else return closest_hit<R>(sc, o, d);
+    else return closest_hit_runs<R, feat_of<ACC>()>(sc, o, d);
 }
 
 template <class R>
@@ -1221,24 +1238,24 @@ RT_HD void set_face(Hit<R>& h, V3<R> d, V3<R> outward) {       // math.js:55-58
     h.n = h.front ? outward : outward * (R)-1;
 }
 
-// Rebuild the HitRecord of the winning primitive (point = origin + dir*t, math.js:41).  LEAN: a sphere
-// (the only primitive a lean scene has)
-template <class R, bool LEAN = false>
+// Rebuild the HitRecord of the winning primitive (point = origin + dir*t, math.js:41).  FEAT: the kinds a
+// scene without the missing features cannot hit are left out
+template <class R, int FEAT = F_ALL>
 RT_HD Hit<R> hit_record(const SceneView<R>& sc, V3<R> o, V3<R> d, const Closest<R>& c) {
     Hit<R> h;
     h.p = o + d * c.t;
     h.mat = c.mat;
-    if (LEAN || c.kind == HIT_SPHERE) {
+    if ((FEAT & (F_PLANES | F_BOXES | F_TRIS)) == 0 || c.kind == HIT_SPHERE) {
         const SphereRec<R> s = sc.spheres[c.idx];
 #if RT_DIV_RCP
         set_face(h, d, vdiv_rcp(h.p - mk(s.cx, s.cy, s.cz), sc.sphere_r[c.idx], sc.sphere_inv_r[c.idx]));
 #else
         set_face(h, d, vdiv(h.p - mk(s.cx, s.cy, s.cz), sc.sphere_r[c.idx]));
 #endif
-    } else if (c.kind == HIT_PLANE) {
+    } else if ((FEAT & F_PLANES) != 0 && c.kind == HIT_PLANE) {
         const PlaneRec<R> p = sc.planes[c.idx];
         set_face(h, d, mk(p.nx, p.ny, p.nz));
-    } else if (c.kind == HIT_BOX) {                                                   // geometry.js:118-126
+    } else if ((FEAT & F_BOXES) != 0 && c.kind == HIT_BOX) {                          // geometry.js:118-126
         const BoxRec<R> b = sc.boxes[c.idx];
         const R eps = (R)1e-6;
         V3<R> n;
@@ -1344,10 +1361,10 @@ __host__ __device__ RT_COLD V3<R> background_procedural(const SceneView<R>& sc, 
 }
 
 // unit: normalize(d), computed by the caller (shade_segment shares it with the scatter of other lanes)
-template <class R, bool LEAN = false>
+template <class R, int FEAT = F_ALL>
 __host__ __device__ V3<R> background(const SceneView<R>& sc, V3<R> d, V3<R> unit) {
     const R I = sc.sky_intensity;
-    if constexpr (LEAN) {                                                             // skyGradient only
+    if constexpr ((FEAT & F_BGALL) == 0) {                                            // skyGradient only
         R t = (R)0.5 * (unit.y + (R)1);
         return (mk<R>(1, 1, 1) * ((R)1 - t) + mk<R>(0.5, 0.7, 1.0) * t) * I;
     }

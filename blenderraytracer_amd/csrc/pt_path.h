@@ -53,7 +53,7 @@ RT_COLD_HD AaUv<R> stochastic_uv(uint32_t key, int i, int j, int width, int heig
 #endif
 // The camera ray (camera.js:38-51) from the camera's 22 words at cp (SceneView: cam_o, cam_llc, cam_h,
 // cam_v, cam_u, cam_vv, cam_w, lens_radius, contiguous)
-template <class R, class P, bool LEAN = false>
+template <class R, class P, int FEAT = F_ALL>
 RT_HD void camera_ray(const SceneView<R>& sc, R u, R v, Rng<R>& g, V3<R>& o, V3<R>& d, P cp) {
     const V3<R> co = mk<R>(cp[0], cp[1], cp[2]);
     const V3<R> llc = mk<R>(cp[3], cp[4], cp[5]);
@@ -62,7 +62,7 @@ RT_HD void camera_ray(const SceneView<R>& sc, R u, R v, Rng<R>& g, V3<R>& o, V3<
     const V3<R> cu = mk<R>(cp[12], cp[13], cp[14]);
     const V3<R> cv = mk<R>(cp[15], cp[16], cp[17]);
     V3<R> rd = random_in_unit_disk(g) * (R)cp[21];
-    if (!LEAN && sc.cam_ortho) {
+    if ((FEAT & F_CAMALL) != 0 && sc.cam_ortho) {
         o = (co + cu * rd.x) + cv * rd.y;
         d = normalize((((llc + hor * u) + ver * v) - o) + mk<R>(cp[18], cp[19], cp[20]) * (R)-1);
     } else {
@@ -79,8 +79,8 @@ RT_HD void camera_ray(const SceneView<R>& sc, R u, R v, Rng<R>& g, V3<R>& o, V3<
 #ifndef RT_CAM_RELOAD
 #define RT_CAM_RELOAD 1
 #endif
-// LEAN (ACC_GRID_LDS_LEAN): supersampling AA and the perspective camera only
-template <class R, bool RELOAD = false, bool LEAN = false>
+// FEAT without F_CAMALL (the lean kernels): supersampling AA and the perspective camera only
+template <class R, bool RELOAD = false, int FEAT = F_ALL>
 RT_HD void start_sample(const SceneView<R>& sc, const ImageParams& im, int i, int j, uint32_t pkey, int s, Rng<R>& g,
                         V3<R>& o, V3<R>& d) {
     RT_HCOUNT(HC_SAMPLES, 1);
@@ -96,7 +96,7 @@ RT_HD void start_sample(const SceneView<R>& sc, const ImageParams& im, int i, in
 #else
     const R width = (R)im.width, height = (R)im.height;
 #endif
-    if (LEAN) {
+    if ((FEAT & F_CAMALL) == 0) {
         u = ((R)i + g.next()) / width;
         v = ((R)j + g.next()) / height;
     } else if (im.aa_mode == 1) {
@@ -120,11 +120,11 @@ RT_HD void start_sample(const SceneView<R>& sc, const ImageParams& im, int i, in
         typedef const __attribute__((address_space(4))) char* ArgPtr;
         CamPtr cp = (CamPtr)((ArgPtr)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(SceneView<R>, cam_o));
         asm volatile("" : "+s"(cp));
-        camera_ray<R, CamPtr, LEAN>(sc, u, v, g, o, d, cp);
+        camera_ray<R, CamPtr, FEAT>(sc, u, v, g, o, d, cp);
         return;
     }
 #endif
-    camera_ray<R, const R*, LEAN>(sc, u, v, g, o, d, &sc.cam_o[0]);
+    camera_ray<R, const R*, FEAT>(sc, u, v, g, o, d, &sc.cam_o[0]);
 }
 
 // x^5 for Schlick's approximation (materials.js:79-83, Math.pow(1 - cosine, 5)), correctly rounded.
@@ -236,7 +236,7 @@ struct PixelResult { uint32_t segments, draws; Work work; uint64_t cyc[3]; };
 // Shade the segment whose closest hit is c (rayColor's body after world.hit, ray-tracer.js:106-122):
 // emission / scatter / background.  Returns true when the sample's path ended; its radiance L is
 // then in `L`, otherwise (o, d, T, depth) describe the next segment.
-template <class R, bool LEAN = false>
+template <class R, int FEAT = F_ALL>
 RT_HD bool shade_segment(const SceneView<R>& sc, const Closest<R>& c, V3<R>& o, V3<R>& d, V3<R>& T, int& depth,
                          Rng<R>& g, V3<R>& L, const MatRec<R>* mats = nullptr) {
     bool done = true;
@@ -246,7 +246,7 @@ RT_HD bool shade_segment(const SceneView<R>& sc, const Closest<R>& c, V3<R>& o, 
     MatRec<R> m{};
     V3<R> p = mk<R>(0, 0, 0);
     if (hit) {
-        h = hit_record<R, LEAN>(sc, o, d, c);
+        h = hit_record<R, FEAT>(sc, o, d, c);
         m = mats ? mats[h.mat] : sc.mats[h.mat];            // mats: an LDS copy (RT_MAT_LDS A/B)
         if (m.type <= 1) p = random_in_unit_sphere(g);                       // Lambertian / Metal's only draws
     }
@@ -268,7 +268,7 @@ RT_HD bool shade_segment(const SceneView<R>& sc, const Closest<R>& c, V3<R>& o, 
         }
     } else {
         RT_HCOUNT(HC_MISS, 1);
-        const V3<R> bg = background<R, LEAN>(sc, d, unit);                    // world.background(ray)
+        const V3<R> bg = background<R, FEAT>(sc, d, unit);                    // world.background(ray)
         L = mk(T.x * bg.x, T.y * bg.y, T.z * bg.z);
     }
     return done;

@@ -81,7 +81,8 @@ constexpr bool dyn_stack() { return sizeof(R) == 4 || (RT_F64_DYN_STACK != 0 && 
 // walks with a per-lane LDS stack (the ordered BVH walks)
 template <int ACC>
 constexpr bool uses_stack() {
-    return ACC == ACC_BVH_STACK || ACC == ACC_BVH_SPHERES || ACC == ACC_BVH_SPHERES_LDS || ACC == ACC_BVH_TRI_LDS;
+    return ACC == ACC_BVH_STACK || ACC == ACC_BVH_SPHERES || ACC == ACC_BVH_SPHERES_LDS || ACC == ACC_BVH_TRI_LDS ||
+           ACC == ACC_BVH_STACK_LEAN;
 }
 
 template <class R, int ACC>
@@ -339,7 +340,7 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
         T = mk<R>(1, 1, 1);
         depth = im.max_depth;
         isegs = 0;
-        start_sample(sc, im, i, j, pkey, s, g, o, d);
+        start_sample<R, false, feat_of<ACC>()>(sc, im, i, j, pkey, s, g, o, d);
     };
     uint32_t next = 64;                       // items [0, 64) are dealt to lanes 0..63 up front
     bool live = (uint32_t)lane < total;
@@ -367,7 +368,7 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
             ++res.segments;
             ++isegs;
             V3<R> L;
-            waiting = shade_segment(sc, c, o, d, T, depth, g, L);
+            waiting = shade_segment<R, feat_of<ACC>()>(sc, c, o, d, T, depth, g, L);
             if (RT_PROFILE) res.cyc[1] += RT_TICK() - t1;
             if (waiting) {
                 if (COUNT) {
@@ -465,7 +466,7 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
         T = mk<R>(1, 1, 1);
         depth = im.max_depth;
         isegs = 0;
-        start_sample<R, sizeof(R) == 4, lean_acc<ACC>()>(sc, im, i, j, pkey, s, g, o, d);
+        start_sample<R, sizeof(R) == 4, feat_of<ACC>()>(sc, im, i, j, pkey, s, g, o, d);
     };
     uint32_t next = 64;                       // items [0, 64) are dealt to lanes 0..63 up front
     bool live = (uint32_t)lane < total;
@@ -480,7 +481,7 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
             ++res.segments;
             ++isegs;
             V3<R> L;
-            waiting = shade_segment<R, lean_acc<ACC>()>(sc, c, o, d, T, depth, g, L, lmats);
+            waiting = shade_segment<R, feat_of<ACC>()>(sc, c, o, d, T, depth, g, L, lmats);
             if (RT_PROFILE) res.cyc[1] += RT_TICK() - t1;
             if (waiting) {
                 if (COUNT) {
@@ -810,11 +811,15 @@ RT_ONEWAVE_INST(double, ACC_BVH)
 RT_ONEWAVE_INST(double, ACC_BVH_STACK)
 RT_ONEWAVE_INST(double, ACC_BVH_SPHERES)
 RT_ONEWAVE_INST(double, ACC_GRID)
+RT_ONEWAVE_INST(double, ACC_BVH_STACK_LEAN)
+RT_ONEWAVE_INST(double, ACC_BRUTE_LEAN)
 RT_ONEWAVE_INST(float, ACC_BRUTE)
 RT_ONEWAVE_INST(float, ACC_BVH)
 RT_ONEWAVE_INST(float, ACC_BVH_STACK)
 RT_ONEWAVE_INST(float, ACC_BVH_SPHERES)
 RT_ONEWAVE_INST(float, ACC_GRID)
+RT_ONEWAVE_INST(float, ACC_BVH_STACK_LEAN)
+RT_ONEWAVE_INST(float, ACC_BRUTE_LEAN)
 #undef RT_ONEWAVE_INST
 #else   // !RT_ONEWAVE_TU: the rest of the file
 
@@ -1162,27 +1167,34 @@ static hipError_t launch_lds_pool(const TraceArgs<R>& a, bool count, double* par
     return register_pool_launch(a.c, dev, qi, (uint32_t)items, stream);
 }
 
-// The lean grid kernel (ACC_GRID_LDS_LEAN) serves this launch: spheres only (a grid scene), no planes or
-// boxes, the sky gradient, the perspective camera, supersampling AA.  RT_LEAN=0: never (A/B)
+// The lean kernels (feat_of, pt_core.h) serve launches whose scene has the sky gradient, the perspective
+// camera and supersampling AA, and the lean kernel's primitives: the grid's (ACC_GRID_LDS_LEAN) spheres
+// alone, the triangle BVH walk's (ACC_BVH_STACK_LEAN) and World order's (ACC_BRUTE_LEAN) no boxes (World
+// order: no triangles either).  RT_LEAN=0: never (A/B); 1 (default): all three; 2: the grid's only
 #ifndef RT_LEAN
 #define RT_LEAN 1
 #endif
 template <class R>
-static bool scene_lean(const SceneView<R>& sc, const ImageParams& im) {
+static bool scene_lean(const SceneView<R>& sc, const ImageParams& im, int feat) {
     static const int v = [] {
         const char* e = getenv("RT_LEAN");
         return e ? atoi(e) : RT_LEAN;
     }();
-    return v != 0 && sc.num_planes == 0 && sc.num_boxes == 0 && sc.num_tri_nodes == 0 && sc.background == 0 &&
-           !sc.cam_ortho && im.aa_mode == 0;
+    if (v == 0 || (v == 2 && feat != 0)) return false;
+    return (sc.num_planes == 0 || (feat & F_PLANES)) && (sc.num_boxes == 0 || (feat & F_BOXES)) &&
+           (sc.num_tri_nodes == 0 || (feat & F_TRIS)) && sc.background == 0 && !sc.cam_ortho && im.aa_mode == 0;
 }
 
 template <class R, int ACC>
 static hipError_t launch_pool_kernel(const TraceArgs<R>& a0, bool count, double* part, int tiles, int chunks,
                                      int chunk, hipStream_t stream) {
-    if constexpr (ACC == ACC_GRID) {
+    if constexpr (ACC == ACC_BRUTE) {
+        if (scene_lean(a0.sc, a0.im, feat_of<ACC_BRUTE_LEAN>()))
+            return launch_onewave_pool<R, ACC_BRUTE_LEAN>(a0, count, part, tiles, chunks, chunk, stream);
+    } else if constexpr (ACC == ACC_GRID) {
         if (const size_t lb = lds_grid_bytes(a0.sc)) {
-            if (scene_lean(a0.sc, a0.im)) return launch_lds_pool<R, ACC_GRID_LDS_LEAN>(a0, count, part, tiles, chunks, chunk, lb, stream);
+            if (scene_lean(a0.sc, a0.im, feat_of<ACC_GRID_LDS_LEAN>()))
+                return launch_lds_pool<R, ACC_GRID_LDS_LEAN>(a0, count, part, tiles, chunks, chunk, lb, stream);
             return launch_lds_pool<R, ACC_GRID_LDS>(a0, count, part, tiles, chunks, chunk, lb, stream);
         }
     } else if constexpr (ACC == ACC_BVH_SPHERES) {
@@ -1194,6 +1206,8 @@ static hipError_t launch_pool_kernel(const TraceArgs<R>& a0, bool count, double*
         if (a.sc.tri_lds_nodes)
             return launch_lds_pool<R, ACC_BVH_TRI_LDS>(a, count, part, tiles, chunks, chunk,
                                                        lds_tri_bytes(a.sc, a.sc.tri_lds_nodes), stream);
+        if (scene_lean(a0.sc, a0.im, feat_of<ACC_BVH_STACK_LEAN>()))
+            return launch_onewave_pool<R, ACC_BVH_STACK_LEAN>(a0, count, part, tiles, chunks, chunk, stream);
     }
     return launch_onewave_pool<R, ACC>(a0, count, part, tiles, chunks, chunk, stream);
 }
@@ -1628,9 +1642,9 @@ __global__ __launch_bounds__(256) void gamma_exceptions_kernel(const double inv_
 
 __global__ __launch_bounds__(64) void preview_kernel(const FinalizeParams p, const double* __restrict__ sum,
                                                      const GammaTable* __restrict__ g, uint8_t* __restrict__ rgba8) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= p.n) return;
     const uint32_t ne = min(g->n_exc, (uint32_t)kGammaExc);
+    // grid-stride (RT_PREVIEW_WGS caps the workgroups; default one per 64 pixels)
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < p.n; q += gridDim.x * blockDim.x) {
     uint32_t o = 255u << 24;
 #pragma unroll 1
     for (int k = 0; k < 3; ++k) {
@@ -1645,6 +1659,7 @@ __global__ __launch_bounds__(64) void preview_kernel(const FinalizeParams p, con
         o |= b << (8 * k);
     }
     *reinterpret_cast<uint32_t*>(rgba8 + 4 * q) = o;
+    }
 }
 
 // A progressive batch's reduce and its running frame in one pass (RT_FUSED_PREVIEW): each thread adds its
@@ -1718,8 +1733,13 @@ hipError_t launch_gamma_thresholds(double gamma, GammaTable* T, hipStream_t stre
 hipError_t launch_finalize(const FinalizeParams& p, const double* sum, double* mean, float* post, uint8_t* rgba8,
                            hipStream_t stream, const GammaTable* thresholds) {
     if (p.n <= 0) return hipSuccess;
+    static const int cap = [] {               // A/B: at most this many preview workgroups (0: no cap)
+        const char* e = getenv("RT_PREVIEW_WGS");
+        return e ? std::max(0, atoi(e)) : 0;
+    }();
     if (thresholds && !mean && !post && rgba8)
-        hipLaunchKernelGGL(preview_kernel, dim3((p.n + 63) / 64), dim3(64), 0, stream, p, sum, thresholds, rgba8);
+        hipLaunchKernelGGL(preview_kernel, dim3(cap ? std::min((p.n + 63) / 64, cap) : (p.n + 63) / 64), dim3(64), 0,
+                           stream, p, sum, thresholds, rgba8);
     else
         hipLaunchKernelGGL(finalize_kernel, dim3((p.n + 63) / 64), dim3(64), 0, stream, p, sum, mean, post, rgba8);
     return hipGetLastError();
