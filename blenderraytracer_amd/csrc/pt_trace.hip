@@ -1667,8 +1667,8 @@ __global__ __launch_bounds__(64) void preview_kernel(const FinalizeParams p, con
 // from the new sums exactly as preview_kernel does (the same binary64 values: identical bytes).  One
 // one-wave workgroup per tile instead of two kernels' (the trace's one-wave workgroups of triangle scenes
 // leave no VGPRs beside them, so every side workgroup takes a trace wave's slot), and the sums are not
-// read a second time.  At most 32 VGPRs (16 waves/SIMD), like the two kernels it replaces.
-__global__ __launch_bounds__(64, 16) void reduce_preview_kernel(const ImageParams im, double* __restrict__ sum,
+// read a second time.  26 VGPRs, like the two kernels it replaces (reduce 16, preview 20).
+__global__ __launch_bounds__(64, 8) void reduce_preview_kernel(const ImageParams im, double* __restrict__ sum,
                                                                 const double* __restrict__ part, const int tiles,
                                                                 const int chunks, const uint32_t* __restrict__ skip,
                                                                 const FinalizeParams p, const GammaTable* __restrict__ g,

@@ -3,7 +3,7 @@
 # pool kernels' VGPRs, spills, scratch, occupancy and LDS.  usage: bash scripts/resource_usage.sh > out.txt
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 echo "# hipcc -O3 -Rpass-analysis=kernel-resource-usage on csrc/pt_trace.hip and pt_onewave.hip ($(git -C $ROOT rev-parse --short HEAD 2>/dev/null))"
-echo "# trace_pool_kernel<R, COUNT, ACC>: ACC 0 brute force, 2 stackless BVH, 3 ordered BVH walk, 4 its sphere-only form; trace_pool_lds_kernel<R, COUNT>: 4 with the nodes in LDS"
+echo "# trace_pool_kernel<R, COUNT, ACC, CANCEL>: ACC 0 brute force, 1 its lean form (spheres + planes), 2 stackless BVH, 3 ordered BVH walk, 10 its lean form (no boxes), 4 the sphere-only walk, 6 the grid; trace_pool_lds_kernel<R, COUNT, ACC>: 5 sphere-tree nodes in LDS, 7 the grid in LDS, 9 its lean form (spheres only), 8 triangle-tree top levels in LDS (opt-in); lean = sky gradient, perspective camera, supersampling only"
 for src in pt_trace.hip pt_onewave.hip; do
   extra=""; [ $src = pt_onewave.hip ] && extra="-mllvm -amdgpu-use-amdgpu-trackers=1"   # as build.py
   echo "## $src $extra"
