@@ -400,6 +400,41 @@ def _render_in_child(script, path, **env):
     return np.load(path)
 
 
+_LEAN_SCRIPT = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import torch  # noqa: F401  (HIP runtime first)
+from blenderraytracer_amd import capi
+from blenderraytracer_amd.renderer import GpuRayTracer
+from blenderraytracer_amd.scene import load_scene_json
+out = {}
+# the three lean kernels' scenes (RTOW: the grid, spheres only; mesh50k: the triangle walk, no boxes;
+# Cornell: World order, spheres and planes), in both precisions, plus a scene that takes none (stochastic AA)
+for name, w, h, crop, aa in (("rtow.json", 160, 90, None, "supersampling"), ("mesh50k", 1920, 1080, (900, 480, 64, 48), "supersampling"),
+                             ("cornell.json", 96, 96, None, "supersampling"), ("rtow.json", 96, 54, None, "stochastic")):
+    for prec in (capi.RT_PREC_F64, capi.RT_PREC_F32):
+        rt = GpuRayTracer(w, h, seed=21, precision=prec)
+        assert rt.load_from_json(load_scene_json(name))
+        rt.update_render_settings({"samples": 6, "maxBounces": 5, "antiAliasing": aa})
+        r = rt.render(crop=crop, want=("mean", "segments", "draws"), batch_samples=2)
+        for k in ("mean", "segments", "draws"):
+            out[f"{name}.{aa}.{prec}.{k}"] = r[k]
+        rt.close()
+np.savez(sys.argv[2], **out)
+'''
+
+
+def test_lean_kernels_bit_identical(gpu, tmp_path):
+    """The lean kernels (round 6: compiled without the plane / box / triangle code a scene cannot use,
+    the other backgrounds, the orthographic camera and the other AA modes) give the general kernels' bits:
+    the same renders with RT_LEAN=0 (never lean) equal the default ones bit for bit, per-pixel segment and
+    RNG-draw counts included — one-shot and in progressive batches, binary64 and binary32."""
+    lean = _render_in_child(_LEAN_SCRIPT, tmp_path / "lean.npz")
+    general = _render_in_child(_LEAN_SCRIPT, tmp_path / "general.npz", RT_LEAN="0")
+    for k in lean.files:
+        assert np.array_equal(lean[k], general[k], equal_nan=True), k
+
+
 @pytest.mark.parametrize("walk", ["skip", "tree", "grid"])
 def test_alternative_bvh_walks_bit_identical(gpu, tmp_path, walk):
     """Every walk renders the same bits as the general two-child walk (RT_BVH_WALK=two): skip = the
