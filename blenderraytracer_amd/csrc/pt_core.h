@@ -1118,9 +1118,14 @@ RT_HD void copy_grid_lds(const SceneView<R>& sc, rt_u4* grec, int* gcell, int t,
     for (int k = t; k <= sc.num_grid_cells; k += threads) gcell[k] = sc.grid_cell[k];
 }
 
+// The grid's walk parameters as the walk reads them (SceneView grid_n .. grid_far)
+struct GridRefs { const int* n; const float *lo, *hi, *cs, *ics; float far; };
+
 // LDSG: the cell offsets and records come from their LDS copy in stk (ACC_GRID_LDS)
 // FEAT: the scene features compiled in (Feat; the grid's lean kernel: spheres only)
-template <class R, bool LDSG = false, int FEAT = F_ALL>
+// LOCAL: sc is a local copy (closest_hit_acc's kernel-argument reload): its axis-indexed reads are
+// selects, not a private array indexed per lane
+template <class R, bool LDSG = false, int FEAT = F_ALL, bool LOCAL = false>
 RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, const BvhStack& stk) {
     const R tmin = (R)0.001;
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
@@ -1131,9 +1136,14 @@ RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work
     if constexpr (sizeof(R) == 8) fr = make_filter_ray(o, d);
     if (sc.num_big_spheres > 0) sphere_records(sc.big_spheres, 0, sc.num_big_spheres, o, d, a, fr, tmin, b, tl, w, true, ya);
     if (sc.num_grid_cells <= 0) return b;
+    const GridRefs gp{sc.grid_n, sc.grid_lo, sc.grid_hi, sc.grid_cs, sc.grid_ics, sc.grid_far};
+    auto at = [](const auto* a, int k) {
+        if constexpr (LOCAL) return k == 0 ? a[0] : (k == 1 ? a[1] : a[2]);
+        else return a[k];
+    };
     const float of[3] = {(float)o.x, (float)o.y, (float)o.z};
     const float df[3] = {(float)d.x, (float)d.y, (float)d.z};
-    if (!(fmaxf(fabsf(of[0]), fmaxf(fabsf(of[1]), fabsf(of[2]))) <= sc.grid_far)) {
+    if (!(fmaxf(fabsf(of[0]), fmaxf(fabsf(of[1]), fabsf(of[2]))) <= gp.far)) {
         // far origin (or NaN): every grid sphere once, in cell order (duplicates are harmless)
         sphere_records(sc.grid_leaf, 0, sc.grid_cell[sc.num_grid_cells], o, d, a, fr, tmin, b, tl, w);
         return b;
@@ -1143,7 +1153,7 @@ RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work
         float v = rt_rcp_approx(df[k]);
         if (!(fabsf(v) <= 0x1p126f)) v = copysignf(0x1p126f, df[k]);
         inv[k] = v;
-        const float ta = (sc.grid_lo[k] - of[k]) * v, tb = (sc.grid_hi[k] - of[k]) * v;
+        const float ta = (gp.lo[k] - of[k]) * v, tb = (gp.hi[k] - of[k]) * v;
         t0 = fmaxf(t0, fminf(ta, tb));
         t1 = fminf(t1, fmaxf(ta, tb));
     }
@@ -1157,17 +1167,17 @@ RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work
         // RTOW f32 +2.7 %); binary64 keeps the correctly rounded division, which measured 3 % faster
         // there (register allocation).  RT_GRID_DIV: 1 division / 2 reciprocal in both (A/B)
         const bool by_div = RT_GRID_DIV == 1 || (RT_GRID_DIV == 0 && sizeof(R) == 8);
-        int c = by_div ? (int)floorf((p - sc.grid_lo[k]) / sc.grid_cs[k])
-                       : (int)floorf((p - sc.grid_lo[k]) * sc.grid_ics[k]);
-        c = c < 0 ? 0 : (c >= sc.grid_n[k] ? sc.grid_n[k] - 1 : c);
+        int c = by_div ? (int)floorf((p - gp.lo[k]) / gp.cs[k])
+                       : (int)floorf((p - gp.lo[k]) * gp.ics[k]);
+        c = c < 0 ? 0 : (c >= gp.n[k] ? gp.n[k] - 1 : c);
         cell[k] = c;
         step[k] = df[k] > 0.0f ? 1 : (df[k] < 0.0f ? -1 : 0);
         tmax[k] = step[k] == 0 ? INFINITY
-                               : (sc.grid_lo[k] + (float)(c + (step[k] > 0)) * sc.grid_cs[k] - of[k]) * inv[k];
+                               : (gp.lo[k] + (float)(c + (step[k] > 0)) * gp.cs[k] - of[k]) * inv[k];
     }
     for (;;) {
         RT_COUNT(++w.nodes);
-        const int ci = cell[0] + sc.grid_n[0] * (cell[1] + sc.grid_n[1] * cell[2]);
+        const int ci = cell[0] + gp.n[0] * (cell[1] + gp.n[1] * cell[2]);
         if constexpr (LDSG) {
             sphere_records_lds(stk.grec, sc.grid_leaf, stk.gcell[ci], stk.gcell[ci + 1], o, d, a, fr, tmin, b, tl, w, ya);
         } else {
@@ -1186,9 +1196,9 @@ RT_HD Closest<R> closest_hit_grid(const SceneView<R>& sc, V3<R> o, V3<R> d, Work
         // (zero / NaN direction; t beyond binary32's range is not modelled, as for the BVH)
         if (b.t < (R)tx || !(tx < INFINITY)) break;
         const int nc = cell[ax] + step[ax];
-        if (nc < 0 || nc >= sc.grid_n[ax]) break;
+        if (nc < 0 || nc >= at(gp.n, ax)) break;
         cell[ax] = nc;
-        tmax[ax] = (sc.grid_lo[ax] + (float)(nc + (step[ax] > 0)) * sc.grid_cs[ax] - of[ax]) * inv[ax];
+        tmax[ax] = (at(gp.lo, ax) + (float)(nc + (step[ax] > 0)) * at(gp.cs, ax) - of[ax]) * inv[ax];
     }
     return b;
 }
@@ -1214,15 +1224,41 @@ template <int ACC> constexpr int feat_of() {
          : ACC == ACC_BRUTE_LEAN ? F_PLANES : F_ALL;
 }
 
-template <class R, int ACC>
+// RT_SC_RELOAD (bit mask of lean kernels: 1 tree, 2 grid, 4 brute force; default 2): the closest-hit
+// query's scene fields read from the kernel-argument segment at every query (a copy the compiler cannot
+// hoist) instead of kept in SGPRs across the segment loop, whose spills it reloads there by VALU
+// v_readlane.  Binary64 only.  Config 3's binary64 grid kernel, with RT_CAM_RELOAD_LEAN64: SGPR spills
+// 55 -> 28, the segment loop's static v_readlanes 24 -> 4, same speed (11,170 vs 11,155 Msamples/s,
+// interleaved); measured and not taken: the tree and brute-force kernels (mesh50k -10 %,
+// Cornell -3.5 %: their waves then wait on the scalar loads, where a v_readlane costs one VALU slot), and
+// binary32 (-1.5 %).  The kernels that instantiate the lean ACCs take the SceneView at offset 0 of their
+// arguments (static_asserts in pt_trace.hip).
+#ifndef RT_SC_RELOAD
+#define RT_SC_RELOAD 2
+#endif
+template <class R, int ACC> constexpr bool sc_reload() {
+    return sizeof(R) == 8 && (((RT_SC_RELOAD & 1) && ACC == ACC_BVH_STACK_LEAN) ||
+                              ((RT_SC_RELOAD & 2) && ACC == ACC_GRID_LDS_LEAN) || ((RT_SC_RELOAD & 4) && ACC == ACC_BRUTE_LEAN));
+}
+// LOCAL: sc is closest_hit_acc's own reloaded copy
+template <class R, int ACC, bool LOCAL = false>
 RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (!LOCAL && sc_reload<R, ACC>()) {
+        typedef const __attribute__((address_space(4))) SceneView<R>* SvPtr;
+        SvPtr p = (SvPtr)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(p));
+        const SceneView<R> scl = *p;
+        return closest_hit_acc<R, ACC, true>(scl, o, d, w, stk);
+    }
+#endif
     if constexpr (ACC == ACC_BVH) return closest_hit_bvh<R, false>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_BVH_STACK) return closest_hit_bvh<R, true>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_BVH_SPHERES) return closest_hit_bvh<R, true, false>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_BVH_SPHERES_LDS) return closest_hit_bvh<R, true, false, true>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_GRID) return closest_hit_grid<R>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_GRID_LDS) return closest_hit_grid<R, true>(sc, o, d, w, stk);
-    else if constexpr (ACC == ACC_GRID_LDS_LEAN) return closest_hit_grid<R, true, feat_of<ACC>()>(sc, o, d, w, stk);
+    else if constexpr (ACC == ACC_GRID_LDS_LEAN) return closest_hit_grid<R, true, feat_of<ACC>(), LOCAL>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_BVH_STACK_LEAN)
         return closest_hit_bvh<R, true, true, false, false, feat_of<ACC>()>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_BVH_TRI_LDS) return closest_hit_bvh<R, true, true, false, true>(sc, o, d, w, stk);

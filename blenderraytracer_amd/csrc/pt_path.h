@@ -75,9 +75,14 @@ RT_HD void camera_ray(const SceneView<R>& sc, R u, R v, Rng<R>& g, V3<R>& o, V3<
 // segment at every sample start (scalar loads through a pointer the compiler cannot hoist) instead of
 // kept live in SGPRs across the segment loop, where the kernel's SGPR spills are reloaded by VALU
 // v_readlane instructions: RTOW f32 +1.6 % (SGPR spills 61 -> 49).  In binary64 the freed SGPRs went to
-// spills inside the walk instead (RTOW -0.3 %, mesh50k -9 %, Cornell -16 %), so binary32 only.
+// spills inside the walk instead (round 5: RTOW -0.3 %, mesh50k -9 %, Cornell -16 %; round 6's lean
+// one-wave kernels: mesh50k -10 %), so binary32 and, with pt_core.h RT_SC_RELOAD, the binary64 lean
+// grid kernel only.
 #ifndef RT_CAM_RELOAD
 #define RT_CAM_RELOAD 1
+#endif
+#ifndef RT_CAM_RELOAD_LEAN64
+#define RT_CAM_RELOAD_LEAN64 1    // the binary64 lean grid kernel reloads too (round 6, with RT_SC_RELOAD)
 #endif
 // FEAT without F_CAMALL (the lean kernels): supersampling AA and the perspective camera only
 template <class R, bool RELOAD = false, int FEAT = F_ALL>

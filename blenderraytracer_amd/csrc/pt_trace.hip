@@ -151,43 +151,50 @@ __device__ __forceinline__ void store_through(double* p, double v) {
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The wave's item of a fused launch is done (the commit protocol of fused batches).  The
-// happens-before chain from a wave's partial stores to the reduce that reads them on another stream:
-//  1. every lane: its partial stores, then an agent-scope release fence (the lanes of a wave are one
-//     instruction stream: the fence orders the wave's stores before lane 0's increment below);
-//  2. lane 0: the batch's item count, a relaxed agent-scope RMW after that fence — the counts of a batch's
-//     items form one release sequence headed by every item's fenced increment;
-//  3. the lane whose increment completes the batch: an agent-scope acquire fence (it has read the last
-//     value of that sequence, so it synchronizes with every other item's release), then the batch's flag
-//     in mapped host memory, a system-scope release store;
+// The wave's item of a fused launch is done (the commit protocol of fused batches): the
+// write-through hand-off of MI355X_MICROARCH.md ("Valid forms", the counter row; cdna_hip_programming.md
+// §6 G16 R1, "sc1 (write-through) stores ... need no release fence"):
+//  1. every lane: its partials stored write-through (store_through: global stores with sc1, which leave
+//     the XCD's L2 and drop the line there), then `s_waitcnt vmcnt(0)` — the wave's stores have completed
+//     at memory (inline asm, which the compiler can neither drop nor move stores across);
+//  2. lane 0, after that wait: the batch's item count, a relaxed agent-scope RMW (performed at memory,
+//     coherent across XCDs);
+//  3. the lane whose increment completes the batch: the batch's flag in mapped host memory, a system-scope
+//     release store (one per batch);
 //  4. the host sees the flag and enqueues the batch's gate, which loads the flag with a system-scope
-//     acquire (reduce_gate_kernel) before it lets the reduce run; the reduce follows the gate in stream
-//     order.
-// On gfx950 the release fence is an L2 write-back (buffer_wbl2 sc1) + vmcnt(0) per item (one; an acq_rel
-// RMW would add a second write-back and an invalidate).  RT_COMMIT_FENCE: 2 (A/B) the acq_rel RMW form;
-// 0 (A/B) round 4's form — an inline `s_waitcnt vmcnt(0)` after the stores and relaxed atomics, correct on
-// gfx950 only because the partial stores are written through (sc1) and complete at the wait
+//     acquire (reduce_gate_kernel); the reduce follows the gate in stream order, in a dispatch of its own
+//     (whose start invalidates the L1s it reads through), and reads the partials from memory.
+// The one-wave kernels (this file compiled as pt_onewave.hip) take this form: a release fence per item is
+// an L2 write-back (buffer_wbl2 sc1) + wait on gfx950, 712k of them per mesh50k frame — 2 % of that frame
+// in progressive batches.  RT_COMMIT_FENCE=1, the LDS pool kernels' form: also an
+// agent-scope release fence before the count (the write-through form gave config 3's LDS kernel a
+// register allocation 2.3 % slower, measured interleaved) and an acquire fence before the flag.
 #ifndef RT_COMMIT_FENCE
+#ifdef RT_ONEWAVE_TU
+#define RT_COMMIT_FENCE 0
+#else
 #define RT_COMMIT_FENCE 1
+#endif
 #endif
 __device__ __forceinline__ void item_done(const Counters& c, int b, uint32_t batch_items, int ways, int lane) {
 #if RT_COMMIT_FENCE
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
-        const uint32_t k = __hip_atomic_fetch_add(c.batch_count + b, 1u, RT_COMMIT_FENCE == 2 ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t k = __hip_atomic_fetch_add(c.batch_count + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k + 1 == batch_items) {
-            if (RT_COMMIT_FENCE != 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             __hip_atomic_store(c.batch_flag + b * (ways > 1 ? ways : 1), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 #else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
         const uint32_t k = __hip_atomic_fetch_add(c.batch_count + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k + 1 == batch_items)
-            __hip_atomic_store(c.batch_flag + b * (ways > 1 ? ways : 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(c.batch_flag + b * (ways > 1 ? ways : 1), 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 #endif
 }
@@ -466,7 +473,7 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
         T = mk<R>(1, 1, 1);
         depth = im.max_depth;
         isegs = 0;
-        start_sample<R, sizeof(R) == 4, feat_of<ACC>()>(sc, im, i, j, pkey, s, g, o, d);
+        start_sample<R, sizeof(R) == 4 || (RT_CAM_RELOAD_LEAN64 != 0 && ACC == ACC_GRID_LDS_LEAN), feat_of<ACC>()>(sc, im, i, j, pkey, s, g, o, d);
     };
     uint32_t next = 64;                       // items [0, 64) are dealt to lanes 0..63 up front
     bool live = (uint32_t)lane < total;
@@ -676,7 +683,7 @@ void trace_pool_lds_kernel(const TraceArgs<R> args, double* __restrict__ part, c
 }
 
 // RT_CAM_RELOAD (pt_path.h start_sample) reads the camera words at offsetof(SceneView, cam_o) of the
-// kernel-argument segment: that holds only while the LDS pool kernel's first parameter is TraceArgs<R>
+// kernel-argument segment (RT_SC_RELOAD, pt_core.h closest_hit_acc, the whole SceneView likewise): that holds only while the LDS pool kernel's first parameter is TraceArgs<R>
 // by value (whose first member is the SceneView, static_assert above).  A signature change fails here
 // instead of reading the camera from the wrong bytes.
 template <class F> struct FirstParam;
@@ -684,8 +691,12 @@ template <class A0, class... As> struct FirstParam<void (*)(A0, As...)> { using 
 static_assert(std::is_same<FirstParam<decltype(&trace_pool_lds_kernel<float, false, ACC_GRID_LDS>)>::type,
                            TraceArgs<float>>::value &&
               std::is_same<FirstParam<decltype(&trace_pool_lds_kernel<float, true, ACC_BVH_SPHERES_LDS>)>::type,
-                           TraceArgs<float>>::value,
-              "the camera reload needs TraceArgs as the LDS pool kernel's first (by-value) argument");
+                           TraceArgs<float>>::value &&
+              std::is_same<FirstParam<decltype(&trace_pool_lds_kernel<double, false, ACC_GRID_LDS_LEAN>)>::type,
+                           TraceArgs<double>>::value &&
+              std::is_same<FirstParam<decltype(&trace_pool_kernel<double, false, ACC_BVH_STACK_LEAN, false>)>::type,
+                           TraceArgs<double>>::value,
+              "the camera and grid reloads need TraceArgs as the LDS pool kernel's first (by-value) argument");
 
 // sum[q] += part[c][tile][.][m] for c = 0 .. chunks-1 in chunk order (binary64); one thread per pixel,
 // one one-wave workgroup per tile (its reads of one chunk are 3 x 512 contiguous bytes).  One-wave
@@ -716,9 +727,8 @@ __global__ __launch_bounds__(64) void reduce_gate_kernel(const ReduceGate g) {
     if (threadIdx.x != 0) return;
     const uint32_t a = __hip_atomic_load(const_cast<uint32_t*>(g.aborted), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint32_t s = __hip_atomic_load(g.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    // a fused batch's flag: the acquire end of item_done's release chain (the partials the reduce reads)
-    const uint32_t f = g.complete ? __hip_atomic_load(g.complete, RT_COMMIT_FENCE ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_SYSTEM) : 1u;
+    // a fused batch's flag: the acquire end of item_done's hand-off (the partials the reduce reads)
+    const uint32_t f = g.complete ? __hip_atomic_load(g.complete, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) : 1u;
     const uint32_t skip = (a | s) || !f ? 1u : 0u;
     *g.skip = skip;
     if (skip) __hip_atomic_store(g.stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
