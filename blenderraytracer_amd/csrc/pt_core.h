@@ -216,17 +216,6 @@ struct BvhNode { float lo[3]; int skip; float hi[3]; int fc; };
 // Bounds interleaved by child (lo[axis][child]) so both children's planes of an axis form one float2:
 // the slab test is 6 packed FMAs (v_pk_fma_f32) per node.
 struct Bvh2Node { float lo[3][2]; float hi[3][2]; int child[2]; int pad[2]; };
-// The same node with its two child boxes quantized to 8 bits per plane against the node's own box
-// (RT_QNODE, the triangle tree; scene_pack.h quantize_node): plane k of child c on axis a decodes to
-// fma((float)q[c][k], 2^(ex[a] - 127), org[a]) in binary32 — the builder picks q so that the decoded box
-// contains the child's box (lo rounded down, hi up, checked with the same fma), so the walk enters every
-// box it entered before (a superset, RN being monotonic: same closest hits).  36 B instead of 64 B.
-// #include <cstdint> types only: host and device share the layout.
-struct QNode { float org[3]; unsigned char ex[4]; unsigned char q[2][6]; int child[2]; };
-static_assert(sizeof(QNode) == 36, "QNode layout");
-#ifndef RT_QNODE
-#define RT_QNODE 0
-#endif
 #ifndef RT_BVH_STACK
 #define RT_BVH_STACK 24           // 6 KB of LDS per one-wave workgroup; trees up to ~16.7M primitives
 #endif
@@ -265,7 +254,6 @@ struct SceneView {
     const TriFilter* tri_filter;   // binary64: the triangle leaves' binary32 pre-filter records (same order)
     const Bvh2Node* sphere_wide;   // two-child nodes of the two trees (preorder)
     const Bvh2Node* tri_wide;
-    const QNode* tri_qnode;        // tri_wide quantized (RT_QNODE), same indices; null if not quantizable
     int num_sphere_wide, num_tri_wide;
     int tri_lds_nodes;             // ACC_BVH_TRI_LDS: the triangle tree's nodes [0, tri_lds_nodes) are read
                                    // from the workgroup's LDS copy (set per launch, pt_trace.hip)
@@ -777,37 +765,6 @@ __device__ __forceinline__ Bvh2Node load_node(__amdgpu_buffer_rsrc_t rs, int i) 
 }
 #endif
 
-// A quantized node's child boxes in binary32 (QNode)
-RT_HD Bvh2Node qnode_decode(const QNode& q) {
-    Bvh2Node n;
-    for (int a = 0; a < 3; ++a) {
-        float sc;
-        const int bits = (int)q.ex[a] << 23;
-        memcpy(&sc, &bits, 4);
-        for (int c = 0; c < 2; ++c) {
-            n.lo[a][c] = fmaf((float)q.q[c][a], sc, q.org[a]);
-            n.hi[a][c] = fmaf((float)q.q[c][3 + a], sc, q.org[a]);
-        }
-    }
-    n.child[0] = q.child[0];
-    n.child[1] = q.child[1];
-    return n;
-}
-#if defined(__HIP_DEVICE_COMPILE__)
-// quantized node i (36 B: two 16-B reads and one 4-B read)
-__device__ __forceinline__ QNode load_qnode(__amdgpu_buffer_rsrc_t rs, int i) {
-    const int off = i * (int)sizeof(QNode);
-    uint32_t q[9];
-    const rt_u4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-    const rt_u4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0);
-    q[0] = a.x; q[1] = a.y; q[2] = a.z; q[3] = a.w; q[4] = b.x; q[5] = b.y; q[6] = b.z; q[7] = b.w;
-    q[8] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 32, 0, 0);
-    QNode n;
-    memcpy(&n, q, sizeof n);
-    return n;
-}
-#endif
-
 // node i from its LDS copy (three 16-B box reads, one 8-B reference read)
 RT_HD Bvh2Node load_node_lds(const BvhStack& s, int i) {
     rt_u4 q[4];
@@ -831,15 +788,13 @@ RT_HD Bvh2Node load_node_lds(const BvhStack& s, int i) {
 // ACC_BVH_SPHERES_LDS); 2 nodes [0, stk.ntop) from the LDS copy, the others from global memory (the
 // triangle tree's top levels, ACC_BVH_TRI_LDS).  Wave-uniform steps read the node with scalar loads in
 // every mode.
-// QN: the nodes are QNode (qwide; RT_QNODE, LDSN 0 only), decoded before the same slab test.
-template <bool WIDE, int LDSN = 0, class Leaf, bool QN = false>
+template <bool WIDE, int LDSN = 0, class Leaf>
 RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const BvhRay& br, const float& tl,
-                    BvhStack stk, Work& w, Leaf&& leaf, const QNode* qwide = nullptr) {
-    static_assert(!QN || LDSN == 0, "quantized nodes are read from global memory only");
+                    BvhStack stk, Work& w, Leaf&& leaf) {
     if constexpr (WIDE) {
         int sp = 0, cur = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
-        const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(QN ? (void*)qwide : (void*)wide, (short)0, 0x7FFFFFFF, 0x00020000);
+        const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)wide, (short)0, 0x7FFFFFFF, 0x00020000);
 #endif
         // true: descend to the new cur
         auto step = [&](const Bvh2Node& n) -> bool {
@@ -890,12 +845,9 @@ RT_HD void bvh_walk(const BvhNode* nodes, int count, const Bvh2Node* wide, const
                         else n = load_node(wrs, cur);
                         down = step(n);
                     }
-                } else if constexpr (QN) {
-                    down = __ballot(cur != first) == 0 ? step(qnode_decode(qwide[first])) : step(qnode_decode(load_qnode(wrs, cur)));
                 } else down = __ballot(cur != first) == 0 ? step(wide[first]) : step(load_node(wrs, cur));
 #else
-                if constexpr (QN) down = step(qnode_decode(qwide[cur]));
-                else down = step(LDSN == 1 || (LDSN == 2 && cur < stk.ntop) ? load_node_lds(stk, cur) : wide[cur]);
+                down = step(LDSN == 1 || (LDSN == 2 && cur < stk.ntop) ? load_node_lds(stk, cur) : wide[cur]);
 #endif
                 if (down) continue;
             } else {
@@ -1031,10 +983,7 @@ RT_HD void tri_leaf_filtered(const SceneView<R>& sc, int fc, const TriRay& tr, V
 // TRI = false (ACC_BVH_SPHERES): scenes without triangles; the triangle walk's code is left out.
 // LDSN: the sphere tree's nodes are read from their LDS copy in stk (ACC_BVH_SPHERES_LDS).
 // TLDS: the triangle tree's top levels are read from their LDS copy in stk (ACC_BVH_TRI_LDS).
-// QNODES: the triangle tree as QNode (RT_QNODE 1: the lean kernels; 2: every walk — host event counts
-// only, tests/hostcheck; sc.tri_qnode must be set)
-template <class R, bool WIDE, bool TRI = true, bool LDSN = false, bool TLDS = false, int FEAT = F_ALL,
-          bool QNODES = ((RT_QNODE == 2 || (RT_QNODE != 0 && FEAT != F_ALL)) && !TLDS)>
+template <class R, bool WIDE, bool TRI = true, bool LDSN = false, bool TLDS = false, int FEAT = F_ALL>
 RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
     const R tmin = (R)0.001;
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
@@ -1052,18 +1001,13 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
             bvh_walk<WIDE, LDSN ? 1 : 0>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w, leaf);
     }
     if (TRI && sc.num_tri_nodes > 0) {
-        // the lean kernels walk the quantized triangle tree (RT_QNODE; pt_trace.hip routes only scenes
-        // whose tree quantized to them)
-        constexpr bool QN = QNODES && WIDE;
         if constexpr (sizeof(R) == 8 && RT_TRI_FILTER != 0) {
             const TriRay tr = make_tri_ray(o, d);
             auto leaf = [&](int fc) { tri_leaf_filtered(sc, fc, tr, o, d, tmin, b, tl, w); };
-            bvh_walk<WIDE, TLDS ? 2 : 0, decltype(leaf)&, QN>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, leaf,
-                                                              sc.tri_qnode);
+            bvh_walk<WIDE, TLDS ? 2 : 0>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, leaf);
         } else {
             auto leaf = [&](int fc) { tri_leaf(sc, fc, o, d, tmin, b, tl, w); };
-            bvh_walk<WIDE, TLDS ? 2 : 0, decltype(leaf)&, QN>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, leaf,
-                                                              sc.tri_qnode);
+            bvh_walk<WIDE, TLDS ? 2 : 0>(sc.tri_nodes, sc.num_tri_nodes, sc.tri_wide, br, tl, stk, w, leaf);
         }
     }
     return b;

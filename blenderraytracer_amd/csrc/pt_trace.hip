@@ -1216,8 +1216,7 @@ static hipError_t launch_pool_kernel(const TraceArgs<R>& a0, bool count, double*
         if (a.sc.tri_lds_nodes)
             return launch_lds_pool<R, ACC_BVH_TRI_LDS>(a, count, part, tiles, chunks, chunk,
                                                        lds_tri_bytes(a.sc, a.sc.tri_lds_nodes), stream);
-        // (RT_QNODE: the lean tree kernel walks the quantized tree, which every finite scene has)
-        if (scene_lean(a0.sc, a0.im, feat_of<ACC_BVH_STACK_LEAN>()) && (RT_QNODE == 0 || a0.sc.tri_qnode))
+        if (scene_lean(a0.sc, a0.im, feat_of<ACC_BVH_STACK_LEAN>()))
             return launch_onewave_pool<R, ACC_BVH_STACK_LEAN>(a0, count, part, tiles, chunks, chunk, stream);
     }
     return launch_onewave_pool<R, ACC>(a0, count, part, tiles, chunks, chunk, stream);

@@ -103,7 +103,6 @@ struct DeviceScene {
     DevBuf<TriFilter> tri_filter;
     DevBuf<SphereLeaf<R>> big_sphere_leaf;
     DevBuf<Bvh2Node> sphere_wide, tri_wide;
-    DevBuf<QNode> tri_qnode;
     DevBuf<int> grid_cell;
     DevBuf<SphereLeaf<R>> grid_leaf;
     SceneView<R> view{};
@@ -112,7 +111,7 @@ struct DeviceScene {
         sphere_mat.release(); plane_mat.release(); box_mat.release(); tri_mat.release(); perm.release(); mats.release();
         plane_obj.release(); box_obj.release(); sphere_nodes.release(); tri_nodes.release(); bvh_sphere_leaf.release();
         bvh_tri_leaf.release(); tri_filter.release(); big_sphere_leaf.release();
-        sphere_wide.release(); tri_wide.release(); tri_qnode.release(); grid_cell.release(); grid_leaf.release();
+        sphere_wide.release(); tri_wide.release(); grid_cell.release(); grid_leaf.release();
     }
 };
 
@@ -127,7 +126,7 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     UP(box_mat, hs.box_mat); UP(tri_mat, hs.tri_mat); UP(perm, rec.perm); UP(mats, rec.mats);
     UP(plane_obj, hs.plane_obj); UP(box_obj, hs.box_obj); UP(sphere_nodes, hs.sphere_bvh); UP(tri_nodes, hs.tri_bvh);
     UP(bvh_sphere_leaf, rec.bvh_sphere_leaf); UP(bvh_tri_leaf, rec.bvh_tri_leaf); UP(tri_filter, rec.tri_filter); UP(big_sphere_leaf, rec.big_sphere_leaf); UP(sphere_wide, hs.sphere_wide); UP(tri_wide, hs.tri_wide);
-    UP(tri_qnode, hs.tri_qnode); UP(grid_cell, hs.grid_cell); UP(grid_leaf, rec.grid_leaf);
+    UP(grid_cell, hs.grid_cell); UP(grid_leaf, rec.grid_leaf);
 #undef UP
     if (e != hipSuccess) return fail(RT_ERR_DEVICE, "scene upload: %s", hipGetErrorString(e));
     SceneView<R>& v = ds.view;
@@ -139,7 +138,6 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     v.bvh_sphere_leaf = ds.bvh_sphere_leaf.p; v.bvh_tri_leaf = ds.bvh_tri_leaf.p; v.tri_filter = ds.tri_filter.p;
     v.big_spheres = ds.big_sphere_leaf.p;
     v.sphere_wide = ds.sphere_wide.p; v.tri_wide = ds.tri_wide.p;
-    v.tri_qnode = hs.tri_qnode.empty() ? nullptr : ds.tri_qnode.p;
     v.grid_cell = ds.grid_cell.p; v.grid_leaf = ds.grid_leaf.p;
     fill_view_constants(v, hs, d);
     return RT_OK;

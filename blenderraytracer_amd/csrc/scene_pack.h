@@ -27,7 +27,6 @@ struct HostScene {   // precision-independent staging, binary64 as packed by the
     std::vector<int> sphere_bvh_prims, tri_bvh_prims;
     std::vector<int> big_spheres;                                 // dominant spheres kept out of the tree
     std::vector<Bvh2Node> sphere_wide, tri_wide;                  // the same trees, two-child nodes
-    std::vector<QNode> tri_qnode;                                 // tri_wide quantized (empty: not quantizable)
     std::vector<int> grid_cell, grid_ids;                         // build_grid: cell offsets, sphere ids
     int grid_n[3] = {0, 0, 0};
     float grid_lo[3] = {0, 0, 0}, grid_hi[3] = {0, 0, 0}, grid_cs[3] = {1, 1, 1}, grid_far = 0;
@@ -357,57 +356,6 @@ inline std::vector<Bvh2Node> make_wide(const std::vector<BvhNode>& t, int top = 
     return out;
 }
 
-// A two-child node's child boxes in 8 bits per plane against the node's own box (QNode, pt_core.h): per
-// axis the origin is the box's binary32 low bound and the scale the smallest power of two 2^e with
-// 255 * 2^e >= the extent; each low plane takes the largest q whose decoded value fma(q, 2^e, org) (binary32,
-// the kernel's own arithmetic) is <= the child's bound, each high plane the smallest q whose decoded value
-// is >= it — checked by evaluating that fma here, so the decoded box contains the child's box whatever the
-// rounding.  False (no quantized tree) for non-finite bounds or a scale outside binary32's normal range.
-inline bool quantize_node(const Bvh2Node& w, QNode& out) {
-    QNode q{};
-    for (int a = 0; a < 3; ++a) {
-        const float lo = std::min(w.lo[a][0], w.lo[a][1]), hi = std::max(w.hi[a][0], w.hi[a][1]);
-        if (!std::isfinite(lo) || !std::isfinite(hi) || !(lo <= hi)) return false;
-        const double ext = (double)hi - (double)lo;
-        int e = -126;
-        if (ext > 0) {
-            int x;
-            std::frexp(ext / 255.0, &x);             // ext / 255 < 2^x
-            e = std::max(-126, x);
-        }
-        bool ok = false;
-        for (int tries = 0; tries < 4 && !ok; ++tries, ++e) {
-            if (e > 127) return false;
-            const float sc = std::ldexp(1.0f, e);
-            ok = true;
-            for (int c = 0; c < 2 && ok; ++c) {
-                const float clo = w.lo[a][c], chi = w.hi[a][c];
-                long long ql = (long long)std::floor(((double)clo - (double)lo) / sc);
-                ql = std::min(255LL, std::max(0LL, ql));
-                while (ql > 0 && std::fmaf((float)ql, sc, lo) > clo) --ql;
-                long long qh = (long long)std::ceil(((double)chi - (double)lo) / sc);
-                qh = std::min(255LL, std::max(0LL, qh));
-                while (qh < 255 && std::fmaf((float)qh, sc, lo) < chi) ++qh;
-                if (std::fmaf((float)ql, sc, lo) > clo || std::fmaf((float)qh, sc, lo) < chi) { ok = false; break; }
-                q.q[c][a] = (unsigned char)ql;
-                q.q[c][3 + a] = (unsigned char)qh;
-            }
-            if (ok) { q.org[a] = lo; q.ex[a] = (unsigned char)(e + 127); }
-        }
-        if (!ok) return false;
-    }
-    q.child[0] = w.child[0];
-    q.child[1] = w.child[1];
-    out = q;
-    return true;
-}
-inline std::vector<QNode> quantize_tree(const std::vector<Bvh2Node>& t) {
-    std::vector<QNode> out(t.size());
-    for (size_t i = 0; i < t.size(); ++i)
-        if (!quantize_node(t[i], out[i])) return {};
-    return out;
-}
-
 #ifndef RT_BIG_SPHERES
 #define RT_BIG_SPHERES 4          // at most this many dominant spheres tested before the walk (0: none)
 #endif
@@ -580,7 +528,6 @@ inline void build_bvhs(HostScene& hs) {
     hs.tri_bvh_prims = std::move(tb.order);
     hs.sphere_wide = make_wide(hs.sphere_bvh);
     hs.tri_wide = make_wide(hs.tri_bvh, RT_TRI_TOP_NODES);
-    hs.tri_qnode = quantize_tree(hs.tri_wide);
 }
 
 // The binary32 pre-filter record of a triangle {v0, e1, e2, ...} (binary64, pt_core.h tri_filter_bound):
@@ -778,7 +725,6 @@ inline SceneView<double> host_view(const HostScene& hs, const rt_scene_desc& d, 
     v.tri_filter = rec.tri_filter.data();
     v.big_spheres = rec.big_sphere_leaf.data();
     v.sphere_wide = hs.sphere_wide.data(); v.tri_wide = hs.tri_wide.data();
-    v.tri_qnode = hs.tri_qnode.empty() ? nullptr : hs.tri_qnode.data();
     v.grid_cell = hs.grid_cell.data(); v.grid_leaf = rec.grid_leaf.data();
     fill_view_constants(v, hs, d);
     return v;

@@ -33,7 +33,6 @@ struct HostView {
         v.tri_filter = rec.tri_filter.data();
         v.big_spheres = rec.big_sphere_leaf.data();
         v.sphere_wide = hs.sphere_wide.data(); v.tri_wide = hs.tri_wide.data();
-        v.tri_qnode = hs.tri_qnode.empty() ? nullptr : hs.tri_qnode.data();
         v.grid_cell = hs.grid_cell.data(); v.grid_leaf = rec.grid_leaf.data();
         fill_view_constants(v, hs, *d);
         return hs.bvh_depth <= 64;                   // the host walks use 64-entry stacks
@@ -287,11 +286,8 @@ extern "C" long long ptc_bvh_check(const rt_scene_desc* d, long long n, unsigned
         gs.gcell = grid_cell_copy.data();
         gs.grec = grid_rec_copy.data();
         const Closest<double> gl = grid ? closest_hit_grid<double, true>(v, O, D, w, gs) : c;
-        // the ordered walk over the quantized triangle tree (QNode, RT_QNODE)
-        const Closest<double> q = v.tri_qnode ? closest_hit_bvh<double, true, true, false, false, F_ALL, true>(v, O, D, w, BvhStack{stack, 1})
-                                              : c;
         if (a.kind != HIT_NONE) ++nh;
-        for (const Closest<double>& x : {b, c, g, gl, q}) {
+        for (const Closest<double>& x : {b, c, g, gl}) {
             const bool same = a.kind == x.kind && (a.kind == HIT_NONE || (a.idx == x.idx && a.mat == x.mat &&
                                                                          std::memcmp(&a.t, &x.t, 8) == 0));
             bad += !same;
