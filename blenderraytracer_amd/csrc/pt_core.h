@@ -11,6 +11,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
+#include "js_math.h"
 
 // Path code is __host__ __device__ so that tests/hostcheck can run the kernel's exact per-lane
 // logic on the CPU (test infrastructure only; librt_hip.so has no host execution path).
@@ -28,6 +29,25 @@
 #define RT_COLD_HD __host__ __device__ RT_COLD
 
 namespace rt {
+
+// Math.pow / exp / sin / cos as the reference's V8 computes them (js_math.h) in binary64; the binary32
+// fast mode keeps the device's own
+template <class R> RT_HD R js_pow(R x, R y) {
+    if constexpr (sizeof(R) == 8) return jsm::pow(x, y);
+    else return pow(x, y);
+}
+template <class R> RT_HD R js_exp(R x) {
+    if constexpr (sizeof(R) == 8) return jsm::exp(x);
+    else return exp(x);
+}
+template <class R> RT_HD R js_sin(R x) {
+    if constexpr (sizeof(R) == 8) return jsm::sin(x);
+    else return sin(x);
+}
+template <class R> RT_HD R js_cos(R x) {
+    if constexpr (sizeof(R) == 8) return jsm::cos(x);
+    else return cos(x);
+}
 
 // Host-only event counts for the instruction-floor model: compiled into the host check
 // built with -DRT_HOST_COUNTERS (scripts/floor_counts.py) and nowhere else.
@@ -1373,11 +1393,11 @@ __host__ __device__ RT_COLD V3<R> background_hdri(const SceneView<R>& sc, V3<R> 
     R mask = sd > ((R)1 - (R)0.04) ? (R)1 : (R)0;
     V3<R> sun_c = mk<R>(1.0, 0.95, 0.8) * (mask * (R)20);
     R corona = js_max<R>(0, (sd - ((R)1 - (R)0.2)) / (R)0.2);
-    V3<R> cor_c = mk<R>(1.0, 0.8, 0.6) * (pow(corona, (R)2) * (R)3);
+    V3<R> cor_c = mk<R>(1.0, 0.8, 0.6) * (js_pow<R>(corona, (R)2) * (R)3);
     R y = dir.y;
     V3<R> sky_c = mk<R>(0.3, 0.5, 0.8) * (js_max<R>(0, y * (R)0.5 + (R)0.5) * (R)2);
     V3<R> gnd_c = mk<R>(0.2, 0.15, 0.1) * js_max<R>(0, -y * (R)0.3);
-    V3<R> sc_c = mk<R>(0.8, 0.9, 1.0) * (pow(js_max<R>(0, (R)1 - fabs(y)), (R)2) * (R)0.3);
+    V3<R> sc_c = mk<R>(0.8, 0.9, 1.0) * (js_pow<R>(js_max<R>(0, (R)1 - fabs(y)), (R)2) * (R)0.3);
     return ((((sky_c + gnd_c) + sc_c) + sun_c) + cor_c) * I;
 }
 
@@ -1387,9 +1407,9 @@ __host__ __device__ RT_COLD V3<R> background_procedural(const SceneView<R>& sc, 
     V3<R> dir = normalize(d);
     V3<R> sun = normalize(mk<R>(0.3, 0.6, 0.8));
     R sd = js_max<R>(0, dot(dir, sun));
-    V3<R> sun_c = mk<R>(1.0, 0.95, 0.8) * (pow(sd, (R)512) * (R)10);
+    V3<R> sun_c = mk<R>(1.0, 0.95, 0.8) * (js_pow<R>(sd, (R)512) * (R)10);
     V3<R> sky_c = mk<R>(0.4, 0.7, 1.0) * (js_max<R>(0, dir.y) * (R)0.8);
-    V3<R> glow_c = mk<R>(1.0, 0.8, 0.6) * (exp(-fabs(dir.y) * (R)4) * (R)0.3);
+    V3<R> glow_c = mk<R>(1.0, 0.8, 0.6) * (js_exp<R>(-fabs(dir.y) * (R)4) * (R)0.3);
     V3<R> gnd_c = mk<R>(0.1, 0.15, 0.1) * js_max<R>(0, -dir.y * (R)0.5);
     R cloud = js_max<R>(0, perlin<R>(sc.perm, dir.x * (R)10, dir.y * (R)3 + (R)2, dir.z * (R)10) * (R)0.8 + (R)0.2);
     V3<R> cl_c = mk<R>(0.9, 0.9, 1.0) * (cloud * js_max<R>(0, dir.y) * (R)0.5);

@@ -43,8 +43,8 @@ template <class R>
 RT_COLD_HD AaUv<R> stochastic_uv(uint32_t key, int i, int j, int width, int height) {
     Rng<R> g{key, 0};
     R r1 = g.next(), r2 = g.next();
-    R ox = sqrt(r1) * cos((R)2 * (R)3.141592653589793 * r2);
-    R oy = sqrt(r1) * sin((R)2 * (R)3.141592653589793 * r2);
+    R ox = sqrt(r1) * js_cos<R>((R)2 * (R)3.141592653589793 * r2);       // ray-tracer.js:130-131, V8's Math.cos / sin
+    R oy = sqrt(r1) * js_sin<R>((R)2 * (R)3.141592653589793 * r2);
     return AaUv<R>{((R)i + (R)0.5 + ox * (R)0.5) / (R)width, ((R)j + (R)0.5 + oy * (R)0.5) / (R)height};
 }
 
@@ -132,13 +132,13 @@ RT_HD void start_sample(const SceneView<R>& sc, const ImageParams& im, int i, in
     camera_ray<R, const R*, FEAT>(sc, u, v, g, o, d, &sc.cam_o[0]);
 }
 
-// x^5 for Schlick's approximation (materials.js:79-83, Math.pow(1 - cosine, 5)), correctly rounded.
-// The reference's own Math.pow (V8 in Node 12) is not: it differs from RN(x^5) by 1 ulp in ~9 % of
-// arguments (glibc in 0.08 %; tests/test_js_host.py::test_pow5_vs_v8_math_pow), so this value is not
-// bit-pinned to the reference.  The path only uses it in `reflectance > Math.random()`, whose draws are
-// multiples of 2^-24: a 1-ulp difference flips that decision only if the reflectance is within 1 ulp
-// of such a multiple (none of 100k test arguments; every golden fixture's decisions identical).  The
-// device pow (ocml, <= 1 ulp) costs ~100 binary64 instructions.  Here x^2, x^4, x^5 are carried
+// x^5 for Schlick's approximation (materials.js:79-83, Math.pow(1 - cosine, 5)), correctly rounded —
+// the fast path of schlick_reflects.  The reference's own Math.pow (V8 in Node 12, restated exactly in
+// js_math.h) is not correctly rounded: it differs from RN(x^5) by 1 ulp in ~9.6 % of arguments
+// (tests/test_js_host.py::test_pow5_vs_v8_math_pow).  The path only uses the value in
+// `reflectance > Math.random()`, whose draws are multiples of 2^-24; schlick_reflects takes V8's own pow
+// wherever the reflectance lies within 2^-40 of the draw, so the decision is V8's.  The device pow
+// (ocml, <= 1 ulp) costs ~100 binary64 instructions.  Here x^2, x^4, x^5 are carried
 // as unevaluated sums hi + lo (error-free products by FMA): the pair approximates x^5 to ~2^-100
 // relative, so the single final rounding gives RN(x^5) unless x^5 lies within 2^-100 of a rounding
 // midpoint.  10 binary64 ops; exact for x = 0 and x = 1.  Checked against exact rationals
@@ -153,6 +153,10 @@ RT_HD R pow5_rn(R x) {
     return r + re;
 }
 
+// V8's Math.pow(x, 5) itself (js_math.h): the rare exact path of schlick_reflects (inlined: out of line,
+// its call cost Cornell 4.4 % in spills around it; inlined, config 3 and Cornell measured unchanged)
+RT_HD double js_pow5_exact(double x) { return jsm::pow(x, 5.0); }
+
 // Dielectric.scatter (materials.js:51-83) by value (RT_COLD_DIEL: out of line, so its registers leave the
 // trace kernel's allocation — A/B): the new direction and the RNG's draw count
 template <class R> struct DielOut { V3<R> nd; uint32_t k; };
@@ -164,6 +168,20 @@ template <class R> struct DielOut { V3<R> nd; uint32_t k; };
 #else
 #define RT_DIEL_HD RT_HD
 #endif
+// Schlick's decision `reflectance(cosine, ratio) > Math.random()` (materials.js:64, 79-83) for the draw u.
+// In binary64 the reference decides with V8's Math.pow (js_math.h), which lies within 1 ulp of the
+// correctly rounded pow5_rn on every argument tested (9.6 % differ).  A difference can move the
+// reflectance across the draw only when the two lie within a few ulps; within 2^-40 relative (4096 ulps)
+// the reflectance is recomputed with V8's own pow — out of line, taken about once per 10^5 tests — so
+// the decision is the reference's bit for bit (tests/test_js_host.py::test_schlick_decisions_are_v8s).
+template <class R>
+RT_HD bool schlick_reflects(R r0, R cos_t, R u) {
+    R refl = r0 + ((R)1 - r0) * pow5_rn((R)1 - cos_t);
+    if constexpr (sizeof(R) == 8)
+        if (fabs(refl - u) <= refl * (R)0x1p-40) refl = r0 + ((R)1 - r0) * js_pow5_exact((R)1 - cos_t);
+    return refl > u;
+}
+
 template <class R>
 RT_DIEL_HD DielOut<R> dielectric_scatter(R inv_ior, R ior, R r0f, R r0b, bool front, V3<R> n, V3<R> unit, uint32_t key,
                                          uint32_t k) {
@@ -176,9 +194,7 @@ RT_DIEL_HD DielOut<R> dielectric_scatter(R inv_ior, R ior, R r0f, R r0b, bool fr
     bool reflect_it = ratio * sin_t > (R)1;
     if (!reflect_it) {                                                        // random drawn only if it can refract
         RT_HCOUNT(HC_DIELECTRIC_SCHLICK, 1);
-        const R r0 = front ? r0f : r0b;
-        R refl = r0 + ((R)1 - r0) * pow5_rn((R)1 - cos_t);
-        reflect_it = refl > g.next();
+        reflect_it = schlick_reflects<R>(front ? r0f : r0b, cos_t, g.next());
     }
     if (reflect_it) {
         nd = reflect(unit, n);

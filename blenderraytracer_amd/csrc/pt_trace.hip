@@ -1574,7 +1574,7 @@ __device__ __forceinline__ double post_channel(const FinalizeParams& p, double c
     if (p.tone_map == 1) tm = js_max<double>(0.0, (x * (2.51 * x + 0.03)) / (x * (2.43 * x + 0.59) + 0.14));
     else if (p.tone_map == 2) tm = x;
     else tm = x / (1.0 + x);
-    return pow(js_max<double>(0.0, tm), inv_gamma);
+    return jsm::pow(js_max<double>(0.0, tm), inv_gamma);      // post-processor.js:38, V8's Math.pow (js_math.h)
 }
 
 __global__ __launch_bounds__(64) void finalize_kernel(const FinalizeParams p, const double* __restrict__ sum,
@@ -1599,18 +1599,17 @@ __global__ __launch_bounds__(64) void finalize_kernel(const FinalizeParams p, co
 // for trace waves to exit (measured 0.2 - 7.5 ms per preview, delaying the next batches' reduces on the
 // same stream; a fused launch's waves never exit).  The binary64 pow alone needs 64 VGPRs, so the
 // preview does without it: the byte finalize_kernel stores, floor(255 pow(max(0, tm), 1/gamma)) clamped,
-// is a step function of the tone-mapped value tm, non-decreasing wherever the device pow is monotone, so
+// is a step function of the tone-mapped value tm, non-decreasing wherever the pow is monotone, so
 // it equals the number of thresholds T_k <= tm, T_k (k = 1..255) the least binary64 tm whose byte is >= k
-// (a binary search over the binary64 bit patterns with the device's own pow, gamma_thresholds_kernel).
-// Where the pow is not monotone — measured: 1 value in the +-3000 ulps around the thresholds of gamma 2.2
-// — the count is wrong, and such values can only lie next to a threshold (a pow error of an ulp moves the
+// (a binary search over the binary64 bit patterns with the same pow, gamma_thresholds_kernel).
+// Where the pow is not monotone the count is wrong, and such values can only lie next to a threshold (a pow error of an ulp moves the
 // byte only where 255 pow(tm) is within ulps of an integer): gamma_exceptions_kernel evaluates the byte on
 // the +-kGammaScan ulps around every threshold and records every value whose byte differs from the count;
 // the preview checks those exceptions (none or a few).  The preview computes tm exactly as
 // finalize_kernel (binary64, same operations): the same bytes (tests/test_gpu_parity.py::
 // test_progressive_preview_and_cancel, ::test_preview_thresholds_match_finalize).  NaN tm: byte 0, as to_u8.
 __device__ __forceinline__ uint32_t gamma_byte(double tm, double inv_gamma) {
-    return to_u8(pow(js_max<double>(0.0, tm), inv_gamma));
+    return to_u8(jsm::pow(js_max<double>(0.0, tm), inv_gamma));
 }
 __device__ __forceinline__ uint32_t gamma_count(const double* __restrict__ t, double tm) {
     uint32_t lo = 0, n = 255;            // the number of thresholds <= tm (t ascending; a NaN tm passes none)

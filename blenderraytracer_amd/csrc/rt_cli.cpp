@@ -21,6 +21,7 @@
 
 #include "../../include/rt_hip.h"
 #include "../../include/rt_scene_json.h"
+#include "js_math.h"
 
 namespace {
 
@@ -114,8 +115,8 @@ int main(int argc, char** argv) {
     s.batch_samples = batch;
     if (denoise > 0) {                                       // post-processor.js:55 weights, host exp
         s.denoise = 1;
-        s.denoise_weights[0] = std::exp(-1.0 / (2 * denoise * denoise));
-        s.denoise_weights[1] = std::exp(-2.0 / (2 * denoise * denoise));
+        s.denoise_weights[0] = jsm::exp(-1.0 / (2 * denoise * denoise));   // V8's Math.exp (post-processor.js:60)
+        s.denoise_weights[1] = jsm::exp(-2.0 / (2 * denoise * denoise));
     }
     const size_t n = (size_t)width * height;
     std::vector<uint8_t> rgba(4 * n);

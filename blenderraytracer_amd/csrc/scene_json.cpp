@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/rt_scene_json.h"
+#include "js_math.h"
 #include "pt_core.h"
 #include "scene_pack.h"
 
@@ -287,7 +288,7 @@ Camera make_camera(V from, V at, V vup, double vfov, double aspect, double apert
     c.perspective = type == "perspective";
     c.orthographic = type == "orthographic";
     const double theta = vfov * M_PI / 180;
-    const double h = std::tan(theta / 2);
+    const double h = jsm::tan(theta / 2);                  // V8's Math.tan (camera.js:15; js_math.h)
     const double vh = 2.0 * h;
     const double vw = aspect * vh;
     c.w = vnorm(vsub(from, at));

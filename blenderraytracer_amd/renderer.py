@@ -7,11 +7,11 @@ update_background (:568-585), resize_canvas (:598-614), render(on_progress) (:16
 Randomness: Math.random is replaced by the keyed RNG; `seed` selects the stream.
 """
 import ctypes as C
-import math
 
 import numpy as np
 
 from . import capi
+from .jsmath import js_exp
 from .scene import PackedScene, default_scene, load_from_json, setup_camera, keyed_permutation, js_or, truthy
 
 
@@ -47,7 +47,7 @@ def settings_struct(width, height, samples, max_bounces, anti_aliasing, tone_map
         # post-processor.js:55: Math.exp(-(kx*kx + ky*ky) / (2 * strength * strength)) for kx^2+ky^2 = 1, 2
         st = float(denoise_strength)
         s.denoise = 1
-        s.denoise_weights[:] = (math.exp(-1 / (2 * st * st)), math.exp(-2 / (2 * st * st)))
+        s.denoise_weights[:] = (js_exp(-1 / (2 * st * st)), js_exp(-2 / (2 * st * st)))   # V8's Math.exp (jsmath.py)
     return s
 
 

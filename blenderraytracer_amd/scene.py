@@ -17,6 +17,7 @@ import os
 import numpy as np
 
 from . import capi
+from .jsmath import js_tan
 from .rng import permutation
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -77,7 +78,7 @@ class Camera:
         self.focus_dist = focus_dist
         self.fov = vfov
         theta = vfov * math.pi / 180
-        h = math.tan(theta / 2)
+        h = js_tan(theta / 2)                 # V8's Math.tan (camera.js:15; jsmath.py)
         vh = 2.0 * h
         vw = aspect * vh
         self.w = vnorm(vsub(look_from, look_at))

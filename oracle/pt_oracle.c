@@ -19,6 +19,200 @@
 
 #include "../include/rt_hip.h"
 
+/* ---- V8's Math.pow / Math.exp (Node 12, V8 7.8: v8::base::ieee754::pow / exp) -------------------------
+ * The reference runs on V8, whose Math.exp is fdlibm's e_exp.c and whose Math.pow is fdlibm's e_pow.c
+ * with one change in the last step (z*t1 divided by ((t1 - 2) - (w + z*w)) instead of fdlibm's
+ * z*t1/(t1 - 2) - (w + z*w)).  Restated for the arguments the path produces (x >= 0 or NaN; every use
+ * takes max(0, .) or 1 - cosine with cosine <= 1): equal to Node's Math.pow / Math.exp bit for bit
+ * (tests/test_js_host.py::test_oracle_js_math_vs_v8). */
+static int o_hi(double x) { uint64_t b; memcpy(&b, &x, 8); return (int)(b >> 32); }
+static uint32_t o_lo(double x) { uint64_t b; memcpy(&b, &x, 8); return (uint32_t)b; }
+static double o_setlo(double x, uint32_t l) { uint64_t b; memcpy(&b, &x, 8); b = (b & 0xffffffff00000000ULL) | l; memcpy(&x, &b, 8); return x; }
+static double o_sethi(double x, int h) { uint64_t b; memcpy(&b, &x, 8); b = (b & 0xffffffffULL) | ((uint64_t)(uint32_t)h << 32); memcpy(&x, &b, 8); return x; }
+static double o_d(uint32_t h, uint32_t l) { uint64_t b = ((uint64_t)h << 32) | l; double d; memcpy(&d, &b, 8); return d; }
+
+static double v8_pow(double x, double y) {
+    if (y == 0) return 1.0;
+    if (x != x || y != y) return x + y;
+    if (signbit(x)) return pow(x, y);                 /* never on the path (x >= +0 there) */
+    if (isinf(y)) return x == 1.0 ? y - y : ((x > 1.0) == (y > 0) ? INFINITY : 0.0);
+    if (y == 1.0) return x;
+    if (y == -1.0) return 1.0 / x;
+    if (y == 2.0) return x * x;
+    if (y == 0.5) return sqrt(x);
+    if (x == 0.0 || x == 1.0 || isinf(x)) return y < 0 ? 1.0 / x : x;
+    const double bp[2] = {1.0, 1.5}, dp_h[2] = {0.0, o_d(0x3FE2B803, 0x40000000)}, dp_l[2] = {0.0, o_d(0x3E4CFDEB, 0x43CFD006)};
+    const double two53 = o_d(0x43400000, 0), huge = 1.0e300, tiny = 1.0e-300;
+    const double L1 = o_d(0x3FE33333, 0x33333303), L2 = o_d(0x3FDB6DB6, 0xDB6FABFF), L3 = o_d(0x3FD55555, 0x518F264D),
+                 L4 = o_d(0x3FD17460, 0xA91D4101), L5 = o_d(0x3FCD864A, 0x93C9DB65), L6 = o_d(0x3FCA7E28, 0x4A454EEF);
+    const double P1 = o_d(0x3FC55555, 0x5555553E), P2 = o_d(0xBF66C16C, 0x16BEBD93), P3 = o_d(0x3F11566A, 0xAF25DE2C),
+                 P4 = o_d(0xBEBBBD41, 0xC5D26BF1), P5 = o_d(0x3E663769, 0x72BEA4D0);
+    const double lg2 = o_d(0x3FE62E42, 0xFEFA39EF), lg2_h = o_d(0x3FE62E43, 0), lg2_l = o_d(0xBE205C61, 0x0CA86C39);
+    const double ovt = 8.0085662595372944372e-17;
+    const double cp = o_d(0x3FEEC709, 0xDC3A03FD), cp_h = o_d(0x3FEEC709, 0xE0000000), cp_l = o_d(0xBE3E2FE0, 0x145B01F5);
+    const double ivln2 = o_d(0x3FF71547, 0x652B82FE), ivln2_h = o_d(0x3FF71547, 0x60000000), ivln2_l = o_d(0x3E54AE0B, 0xF85DDF44);
+    double ax = x, t1, t2;
+    int ix = o_hi(x) & 0x7fffffff, iy = o_hi(y) & 0x7fffffff, hy = o_hi(y), n, j, k, i;
+    if (iy > 0x41e00000) {                            /* |y| > 2^31 */
+        if (iy > 0x43f00000) return (ix <= 0x3fefffff) == (hy < 0) ? huge * huge : tiny * tiny;
+        if (ix < 0x3fefffff) return hy < 0 ? huge * huge : tiny * tiny;
+        if (ix > 0x3ff00000) return hy > 0 ? huge * huge : tiny * tiny;
+        double t = ax - 1.0, w = (t * t) * (0.5 - t * (0.3333333333333333333333 - t * 0.25));
+        double u = ivln2_h * t, v = t * ivln2_l - w * ivln2;
+        t1 = o_setlo(u + v, 0);
+        t2 = v - (t1 - u);
+    } else {
+        n = 0;
+        if (ix < 0x00100000) { ax *= two53; n -= 53; ix = o_hi(ax); }
+        n += (ix >> 20) - 0x3ff;
+        j = ix & 0x000fffff;
+        ix = j | 0x3ff00000;
+        if (j <= 0x3988E) k = 0; else if (j < 0xBB67A) k = 1; else { k = 0; n += 1; ix -= 0x00100000; }
+        ax = o_sethi(ax, ix);
+        double u = ax - bp[k], v = 1.0 / (ax + bp[k]), ss = u * v, s_h = o_setlo(ss, 0);
+        double t_h = o_sethi(0.0, ((ix >> 1) | 0x20000000) + 0x00080000 + (k << 18));
+        double t_l = ax - (t_h - bp[k]);
+        double s_l = v * ((u - s_h * t_h) - s_h * t_l);
+        double s2 = ss * ss;
+        double r = s2 * s2 * (L1 + s2 * (L2 + s2 * (L3 + s2 * (L4 + s2 * (L5 + s2 * L6)))));
+        r += s_l * (s_h + ss);
+        s2 = s_h * s_h;
+        t_h = o_setlo(3.0 + s2 + r, 0);
+        t_l = r - ((t_h - 3.0) - s2);
+        u = s_h * t_h;
+        v = s_l * t_h + t_l * ss;
+        double p_h = o_setlo(u + v, 0), p_l = v - (p_h - u);
+        double z_h = cp_h * p_h, z_l = cp_l * p_h + p_l * cp + dp_l[k];
+        double t = (double)n;
+        t1 = o_setlo(((z_h + z_l) + dp_h[k]) + t, 0);
+        t2 = z_l - (((t1 - t) - dp_h[k]) - z_h);
+    }
+    double y1 = o_setlo(y, 0), p_l = (y - y1) * t1 + y * t2, p_h = y1 * t1, z = p_l + p_h;
+    j = o_hi(z); i = (int)o_lo(z);
+    if (j >= 0x40900000) {
+        if (((j - 0x40900000) | i) != 0 || p_l + ovt > z - p_h) return huge * huge;
+    } else if ((j & 0x7fffffff) >= 0x4090cc00) {
+        if ((((uint32_t)j - 0xc090cc00u) | (uint32_t)i) != 0 || p_l <= z - p_h) return tiny * tiny;
+    }
+    i = j & 0x7fffffff; k = (i >> 20) - 0x3ff; n = 0;
+    if (i > 0x3fe00000) {
+        n = j + (0x00100000 >> (k + 1));
+        k = ((n & 0x7fffffff) >> 20) - 0x3ff;
+        double t = o_sethi(0.0, n & ~(0x000fffff >> k));
+        n = ((n & 0x000fffff) | 0x00100000) >> (20 - k);
+        if (j < 0) n = -n;
+        p_h -= t;
+    }
+    double t = o_setlo(p_l + p_h, 0), u = t * lg2_h, v = (p_l - (t - p_h)) * lg2 + t * lg2_l;
+    z = u + v;
+    double w = v - (z - u), tt = z * z;
+    double tz = z - tt * (P1 + tt * (P2 + tt * (P3 + tt * (P4 + tt * P5))));
+    double r = (z * tz) / ((tz - 2.0) - (w + z * w));   /* V8's last step */
+    z = 1.0 - (r - z);
+    j = o_hi(z) + (int)((uint32_t)n << 20);
+    return (j >> 20) <= 0 ? scalbn(z, n) : o_sethi(z, o_hi(z) + (int)((uint32_t)n << 20));
+}
+
+static double v8_exp(double x) {
+    const double huge = 1.0e300, twom1000 = o_d(0x01700000, 0), o_thr = o_d(0x40862E42, 0xFEFA39EF),
+                 u_thr = o_d(0xc0874910, 0xD52D3051), ln2HI = o_d(0x3fe62e42, 0xfee00000),
+                 ln2LO = o_d(0x3dea39ef, 0x35793c76), invln2 = o_d(0x3ff71547, 0x652b82fe);
+    const double P1 = o_d(0x3FC55555, 0x5555553E), P2 = o_d(0xBF66C16C, 0x16BEBD93), P3 = o_d(0x3F11566A, 0xAF25DE2C),
+                 P4 = o_d(0xBEBBBD41, 0xC5D26BF1), P5 = o_d(0x3E663769, 0x72BEA4D0);
+    double hi = 0, lo = 0, c, t, y;
+    int k = 0;
+    uint32_t hx = (uint32_t)o_hi(x);
+    int xsb = (int)(hx >> 31);
+    hx &= 0x7fffffff;
+    if (hx >= 0x40862E42) {
+        if (hx >= 0x7ff00000) return (((hx & 0xfffff) | o_lo(x)) != 0) ? x + x : (xsb == 0 ? x : 0.0);
+        if (x > o_thr) return huge * huge;
+        if (x < u_thr) return twom1000 * twom1000;
+    }
+    if (hx > 0x3fd62e42) {
+        if (hx < 0x3FF0A2B2) { hi = xsb ? x + ln2HI : x - ln2HI; lo = xsb ? -ln2LO : ln2LO; k = 1 - xsb - xsb; }
+        else { k = (int)(invln2 * x + (xsb ? -0.5 : 0.5)); t = k; hi = x - t * ln2HI; lo = t * ln2LO; }
+        x = hi - lo;
+    } else if (hx < 0x3e300000) {
+        if (huge + x > 1.0) return 1.0 + x;
+    } else k = 0;
+    t = x * x;
+    c = x - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    if (k == 0) return 1.0 - ((x * c) / (c - 2.0) - x);
+    y = 1.0 - ((lo - (x * c) / (2.0 - c)) - hi);
+    if (k >= -1021) return o_sethi(y, o_hi(y) + (int)((uint32_t)k << 20));
+    return o_sethi(y, o_hi(y) + (int)((uint32_t)(k + 1000) << 20)) * twom1000;
+}
+/* V8's Math.sin / Math.cos (fdlibm s_sin.c / s_cos.c, k_sin.c, k_cos.c, e_rem_pio2.c), restated for
+ * the stochastic AA's arguments 2 pi r, r in [0, 1) (ray-tracer.js:130-131); |x| beyond 2^19 pi/2 would
+ * take fdlibm's large reduction, which this restatement does not have (glibc there, never on the path). */
+static double v8_ksin(double x, double y, int iy) {
+    const double S1 = o_d(0xBFC55555, 0x55555549), S2 = o_d(0x3F811111, 0x1110F8A6), S3 = o_d(0xBF2A01A0, 0x19C161D5),
+                 S4 = o_d(0x3EC71DE3, 0x57B1FE7D), S5 = o_d(0xBE5AE5E6, 0x8A2B9CEB), S6 = o_d(0x3DE5D93A, 0x5ACFD57C);
+    if ((o_hi(x) & 0x7fffffff) < 0x3e400000 && (int)x == 0) return x;
+    double z = x * x, v = z * x, r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    return iy == 0 ? x + v * (S1 + z * r) : x - ((z * (0.5 * y - v * r) - y) - v * S1);
+}
+static double v8_kcos(double x, double y) {
+    const double C1 = o_d(0x3FA55555, 0x5555554C), C2 = o_d(0xBF56C16C, 0x16C15177), C3 = o_d(0x3EFA01A0, 0x19CB1590),
+                 C4 = o_d(0xBE927E4F, 0x809C52AD), C5 = o_d(0x3E21EE9E, 0xBDB4B1C4), C6 = o_d(0xBDA8FAE9, 0xBE8838D4);
+    int ix = o_hi(x) & 0x7fffffff;
+    if (ix < 0x3e400000 && (int)x == 0) return 1.0;
+    double z = x * x, r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    if (ix < 0x3FD33333) return 1.0 - (0.5 * z - (z * r - x * y));
+    double qx = ix > 0x3fe90000 ? 0.28125 : o_sethi(0.0, ix - 0x00200000);
+    return (1.0 - qx) - ((0.5 * z - qx) - (z * r - x * y));
+}
+static int v8_rem_pio2(double x, double* y) {
+    static const int hw[32] = {0x3FF921FB, 0x400921FB, 0x4012D97C, 0x401921FB, 0x401F6A7A, 0x4022D97C, 0x4025FDBB,
+        0x402921FB, 0x402C463A, 0x402F6A7A, 0x4031475C, 0x4032D97C, 0x40346B9C, 0x4035FDBB, 0x40378FDB, 0x403921FB,
+        0x403AB41B, 0x403C463A, 0x403DD85A, 0x403F6A7A, 0x40407E4C, 0x4041475C, 0x4042106C, 0x4042D97C, 0x4043A28C,
+        0x40446B9C, 0x404534AC, 0x4045FDBB, 0x4046C6CB, 0x40478FDB, 0x404858EB, 0x404921FB};
+    const double invpio2 = o_d(0x3FE45F30, 0x6DC9C883), p1 = o_d(0x3FF921FB, 0x54400000), p1t = o_d(0x3DD0B461, 0x1A626331),
+                 p2 = o_d(0x3DD0B461, 0x1A600000), p2t = o_d(0x3BA3198A, 0x2E037073), p3 = o_d(0x3BA3198A, 0x2E000000),
+                 p3t = o_d(0x397B839A, 0x252049C1);
+    int hx = o_hi(x), ix = hx & 0x7fffffff;
+    if (ix < 0x4002d97c) {                                 /* |x| < 3 pi/4 (callers handle |x| <= pi/4) */
+        double sg = hx > 0 ? 1.0 : -1.0, z = x - sg * p1;
+        if (ix != 0x3ff921fb) { y[0] = z - sg * p1t; y[1] = (z - y[0]) - sg * p1t; }
+        else { z -= sg * p2; y[0] = z - sg * p2t; y[1] = (z - y[0]) - sg * p2t; }
+        return hx > 0 ? 1 : -1;
+    }
+    double t = fabs(x);
+    int n = (int)(t * invpio2 + 0.5);
+    double fn = (double)n, r = t - fn * p1, w = fn * p1t;
+    y[0] = r - w;
+    if (!(n < 32 && ix != hw[n - 1])) {
+        int j = ix >> 20, i = j - ((o_hi(y[0]) >> 20) & 0x7ff);
+        if (i > 16) {
+            t = r; w = fn * p2; r = t - w; w = fn * p2t - ((t - r) - w); y[0] = r - w;
+            i = j - ((o_hi(y[0]) >> 20) & 0x7ff);
+            if (i > 49) { t = r; w = fn * p3; r = t - w; w = fn * p3t - ((t - r) - w); y[0] = r - w; }
+        }
+    }
+    y[1] = (r - y[0]) - w;
+    if (hx < 0) { y[0] = -y[0]; y[1] = -y[1]; return -n; }
+    return n;
+}
+static double v8_sincos(double x, int want_cos) {
+    int ix = o_hi(x) & 0x7fffffff;
+    if (ix <= 0x3fe921fb) return want_cos ? v8_kcos(x, 0.0) : v8_ksin(x, 0.0, 0);
+    if (ix >= 0x7ff00000) return x - x;
+    if (ix > 0x413921fb) return want_cos ? cos(x) : sin(x);
+    double y[2];
+    int n = (v8_rem_pio2(x, y) + want_cos) & 3;            /* cos(x) = sin(x + pi/2) */
+    switch (n) {
+        case 0: return v8_ksin(y[0], y[1], 1);
+        case 1: return v8_kcos(y[0], y[1]);
+        case 2: return -v8_ksin(y[0], y[1], 1);
+        default: return -v8_kcos(y[0], y[1]);
+    }
+}
+void oracle_v8_trig_many(int want_cos, const double* x, double* out, long n) { for (long i = 0; i < n; ++i) out[i] = v8_sincos(x[i], want_cos); }
+/* test hooks (tests/test_js_host.py) */
+void oracle_v8_pow_many(const double* x, const double* y, double* out, long n) { for (long i = 0; i < n; ++i) out[i] = v8_pow(x[i], y[i]); }
+void oracle_v8_exp_many(const double* x, double* out, long n) { for (long i = 0; i < n; ++i) out[i] = v8_exp(x[i]); }
+
 typedef struct { double x, y, z; } V3;
 
 static inline V3 v3(double x, double y, double z) { V3 r = {x, y, z}; return r; }
@@ -212,7 +406,7 @@ static int world_hit(const rt_scene_desc* sc, V3 o, V3 d, double tmin, double tm
 static double schlick(double cosine, double ref_idx) {                                    /* materials.js:79-83 */
     double r0 = (1 - ref_idx) / (1 + ref_idx);
     r0 = r0 * r0;
-    return r0 + (1 - r0) * pow((1 - cosine), 5);
+    return r0 + (1 - r0) * v8_pow((1 - cosine), 5);
 }
 static V3 refract(V3 uv, V3 n, double eta) {                                              /* materials.js:72-77 */
     double cos_t = js_min(vdot(vmul(uv, -1), n), 1.0);
@@ -298,13 +492,13 @@ void orc_background(const rt_scene_desc* sc, const double* d_, double* out) {
         double mask = sd > (1.0 - 0.04) ? 1.0 : 0.0;
         V3 sun_c = vmul(v3(1.0, 0.95, 0.8), mask * 20);
         double corona = js_max(0, (sd - (1.0 - 0.2)) / 0.2);
-        V3 cor_c = vmul(v3(1.0, 0.8, 0.6), pow(corona, 2) * 3);
+        V3 cor_c = vmul(v3(1.0, 0.8, 0.6), v8_pow(corona, 2) * 3);
         double y = dir.y;
         double sky_i = js_max(0, y * 0.5 + 0.5);
         V3 sky_c = vmul(v3(0.3, 0.5, 0.8), sky_i * 2);
         double gb = js_max(0, -y * 0.3);
         V3 gnd_c = vmul(v3(0.2, 0.15, 0.1), gb);
-        double scat = pow(js_max(0, 1.0 - fabs(y)), 2) * 0.3;
+        double scat = v8_pow(js_max(0, 1.0 - fabs(y)), 2) * 0.3;
         V3 sc_c = vmul(v3(0.8, 0.9, 1.0), scat);
         c = vmul(vadd(vadd(vadd(vadd(sky_c, gnd_c), sc_c), sun_c), cor_c), I);
         break;
@@ -313,11 +507,11 @@ void orc_background(const rt_scene_desc* sc, const double* d_, double* out) {
         V3 dir = vnorm(d);
         V3 sun = vnorm(v3(0.3, 0.6, 0.8));
         double sd = js_max(0, vdot(dir, sun));
-        double si = pow(sd, 512);
+        double si = v8_pow(sd, 512);
         V3 sun_c = vmul(v3(1.0, 0.95, 0.8), si * 10);
         double hb = js_max(0, dir.y);
         V3 sky_c = vmul(v3(0.4, 0.7, 1.0), hb * 0.8);
-        double glow = exp(-fabs(dir.y) * 4) * 0.3;
+        double glow = v8_exp(-fabs(dir.y) * 4) * 0.3;
         V3 glow_c = vmul(v3(1.0, 0.8, 0.6), glow);
         V3 gnd_c = vmul(v3(0.1, 0.15, 0.1), js_max(0, -dir.y * 0.5));
         double cloud = js_max(0, orc_perlin(sc->perm, dir.x * 10, dir.y * 3 + 2, dir.z * 10) * 0.8 + 0.2);
@@ -355,8 +549,8 @@ static void aa_sample(int mode, int i, int j, int W, int H, Rng* rng, double* u,
     /* ray-tracer.js:125-149 */
     if (mode == RT_AA_STOCHASTIC) {
         double r1 = rng_next(rng), r2 = rng_next(rng);
-        double ox = sqrt(r1) * cos(2 * M_PI * r2);
-        double oy = sqrt(r1) * sin(2 * M_PI * r2);
+        double ox = sqrt(r1) * v8_sincos(2 * M_PI * r2, 1);   /* V8's Math.cos / Math.sin */
+        double oy = sqrt(r1) * v8_sincos(2 * M_PI * r2, 0);
         *u = (i + 0.5 + ox * 0.5) / W;
         *v = (j + 0.5 + oy * 0.5) / H;
     } else if (mode == RT_AA_SUPERSAMPLING) {
@@ -406,7 +600,7 @@ void orc_tone_map(int mode, double exposure, const double* c, double* out) {
 }
 void orc_gamma(double gamma, const double* c, double* out) {
     double inv = 1.0 / gamma;
-    for (int k = 0; k < 3; k++) out[k] = pow(js_max(0, c[k]), inv);
+    for (int k = 0; k < 3; k++) out[k] = v8_pow(js_max(0, c[k]), inv);
 }
 static uint8_t to_u8(double c) {                                                          /* ray-tracer.js:245-247 */
     double v = js_min(255, js_max(0, floor(c * 255)));

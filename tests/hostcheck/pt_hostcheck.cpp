@@ -355,6 +355,20 @@ extern "C" void ptc_host_counts(unsigned long long* out, int reset) {
 extern "C" void ptc_pow5(const double* x, double* out, long long n) {
     for (long long i = 0; i < n; ++i) out[i] = rt::pow5_rn<double>(x[i]);
 }
+// the kernel's Schlick decision (pt_path.h schlick_reflects) for n (r0, cosine, draw) triples
+extern "C" void ptc_schlick(const double* r0, const double* cos_t, const double* u, uint8_t* out, long long n) {
+    for (long long i = 0; i < n; ++i) out[i] = rt::schlick_reflects<double>(r0[i], cos_t[i], u[i]) ? 1 : 0;
+}
+// the kernel's Math.pow / Math.exp (csrc/js_math.h), host build
+extern "C" void ptc_js_pow(const double* x, const double* y, double* out, long long n) {
+    for (long long i = 0; i < n; ++i) out[i] = jsm::pow(x[i], y[i]);
+}
+extern "C" void ptc_js_exp(const double* x, double* out, long long n) {
+    for (long long i = 0; i < n; ++i) out[i] = jsm::exp(x[i]);
+}
+extern "C" void ptc_js_trig(int f, const double* x, double* out, long long n) {     // 0 sin, 1 cos, 2 tan
+    for (long long i = 0; i < n; ++i) out[i] = f == 0 ? jsm::sin(x[i]) : f == 1 ? jsm::cos(x[i]) : jsm::tan(x[i]);
+}
 
 
 // Grid shape (build_grid): cells per axis and sphere registrations (TEST/DEV TOOL)

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "hostcheck", "pt_hostcheck.cpp")
 DEPS = [SRC] + [os.path.join(ROOT, "blenderraytracer_amd", "csrc", f) for f in ("pt_core.h", "pt_path.h", "scene_pack.h",
-                                                                          "pool_order.h")]
+                                                                          "pool_order.h", "js_math.h")]
 LIB = os.path.join(HERE, "hostcheck", "_build", "libpt_hostcheck.so")
 _lib = None
 

@@ -49,6 +49,28 @@ def test_f64_matches_reference(gpu, case):
     rt.close()
 
 
+@pytest.mark.parametrize("case", gc.case_names())
+def test_f64_sample_order_bit_exact_to_reference(gpu, case):
+    """In the reference's own summation order (rt_settings.sum_order = RT_SUM_SAMPLE_ORDER: each pixel's
+    samples added in sample order, ray-tracer.js:202-206) the GPU's binary64 render IS the reference's:
+    per-pixel linear means, post-gamma values (float32 storage), RGBA8 bytes and the denoised frame
+    equal the fixtures bit for bit — the kernel evaluates Math.pow / exp / sin / cos with V8's own
+    algorithms (csrc/js_math.h) and Schlick's decision exactly (pt_path.h schlick_reflects)."""
+    rt, c = gc.tracer_for(case, precision=capi.RT_PREC_F64)
+    rt.sum_order = capi.RT_SUM_SAMPLE_ORDER
+    r = rt.render(crop=c["crop"], want=WANT)
+    lin = gc.load_array(case, "linear")
+    nan = np.isnan(lin)
+    assert np.array_equal(np.isnan(r["mean"]), nan)
+    assert np.array_equal(r["mean"][~nan], lin[~nan]), f"{int((r['mean'][~nan] != lin[~nan]).sum())} channels differ"
+    assert np.array_equal(r["rgba8"], gc.load_array(case, "rgba8"))
+    ref_post = gc.load_array(case, "denoised")[..., :3] if gc.has(case, "denoised") else gc.load_array(case, "post")
+    ok = ~np.isnan(ref_post)
+    assert np.array_equal(np.isnan(r["post"][..., :3]), ~ok)
+    assert np.array_equal(r["post"][..., :3][ok], ref_post.astype(np.float32)[ok])
+    rt.close()
+
+
 # f32 fast mode: RMS of post-gamma output vs the reference.  At these low sample counts a single
 # flipped path decision moves a pixel by up to 1/spp, so the bounds are per case; the north-star
 # budget (1e-3) is asserted on the 512-spp RTOW crop.
