@@ -153,9 +153,11 @@ RT_HD R pow5_rn(R x) {
     return r + re;
 }
 
-// V8's Math.pow(x, 5) itself (js_math.h): the rare exact path of schlick_reflects (inlined: out of line,
-// its call cost Cornell 4.4 % in spills around it; inlined, config 3 and Cornell measured unchanged)
+// V8's Math.pow(x, 5) itself (js_math.h): the rare exact path of schlick_reflects — inlined (config 3
+// and Cornell unchanged; out of line, the call's register saves cost Cornell 4.4 %) or, in the lean
+// triangle-tree kernel, out of line (inlined cost config 5 0.6 %, out of line nothing)
 RT_HD double js_pow5_exact(double x) { return jsm::pow(x, 5.0); }
+static RT_COLD_HD double js_pow5_exact_ool(double x) { return jsm::pow(x, 5.0); }
 
 // Dielectric.scatter (materials.js:51-83) by value (RT_COLD_DIEL: out of line, so its registers leave the
 // trace kernel's allocation — A/B): the new direction and the RNG's draw count
@@ -174,15 +176,17 @@ template <class R> struct DielOut { V3<R> nd; uint32_t k; };
 // reflectance across the draw only when the two lie within a few ulps; within 2^-40 relative (4096 ulps)
 // the reflectance is recomputed with V8's own pow — out of line, taken about once per 10^5 tests — so
 // the decision is the reference's bit for bit (tests/test_js_host.py::test_schlick_decisions_are_v8s).
-template <class R>
+// OOL: the exact path out of line (js_pow5_exact_ool)
+template <class R, bool OOL = false>
 RT_HD bool schlick_reflects(R r0, R cos_t, R u) {
     R refl = r0 + ((R)1 - r0) * pow5_rn((R)1 - cos_t);
     if constexpr (sizeof(R) == 8)
-        if (fabs(refl - u) <= refl * (R)0x1p-40) refl = r0 + ((R)1 - r0) * js_pow5_exact((R)1 - cos_t);
+        if (fabs(refl - u) <= refl * (R)0x1p-40)
+            refl = r0 + ((R)1 - r0) * (OOL ? js_pow5_exact_ool((R)1 - cos_t) : js_pow5_exact((R)1 - cos_t));
     return refl > u;
 }
 
-template <class R>
+template <class R, bool OOL = false>
 RT_DIEL_HD DielOut<R> dielectric_scatter(R inv_ior, R ior, R r0f, R r0b, bool front, V3<R> n, V3<R> unit, uint32_t key,
                                          uint32_t k) {
     Rng<R> g{key, k};
@@ -194,7 +198,7 @@ RT_DIEL_HD DielOut<R> dielectric_scatter(R inv_ior, R ior, R r0f, R r0b, bool fr
     bool reflect_it = ratio * sin_t > (R)1;
     if (!reflect_it) {                                                        // random drawn only if it can refract
         RT_HCOUNT(HC_DIELECTRIC_SCHLICK, 1);
-        reflect_it = schlick_reflects<R>(front ? r0f : r0b, cos_t, g.next());
+        reflect_it = schlick_reflects<R, OOL>(front ? r0f : r0b, cos_t, g.next());
     }
     if (reflect_it) {
         nd = reflect(unit, n);
@@ -214,7 +218,7 @@ RT_DIEL_HD DielOut<R> dielectric_scatter(R inv_ior, R ior, R r0f, R r0b, bool fr
 // branch (RTOW +3.8 %), and the one normalize each material needs — Lambertian the unit-sphere point
 // `p`, Metal and Dielectric the ray direction — arrives as `unit`, computed by shade_segment together
 // with the missed rays' (skyGradient's) normalize (+1.6 %).
-template <class R>
+template <class R, bool OOL = false>
 RT_HD bool scatter(const MatRec<R>& m, const Hit<R>& h, V3<R> unit, V3<R> p, Rng<R>& g, V3<R>& nd, V3<R>& att) {
     if (m.type <= 1) {
         att = mk(m.c[0], m.c[1], m.c[2]);
@@ -234,7 +238,7 @@ RT_HD bool scatter(const MatRec<R>& m, const Hit<R>& h, V3<R> unit, V3<R> p, Rng
     return true;
 #endif
     // Dielectric :51-83 (ior)
-    const DielOut<R> r = dielectric_scatter<R>(m.c[0], m.p, m.c[1], m.c[2], h.front, h.n, unit, g.key, g.k);
+    const DielOut<R> r = dielectric_scatter<R, OOL>(m.c[0], m.p, m.c[1], m.c[2], h.front, h.n, unit, g.key, g.k);
     nd = r.nd;
     g.k = r.k;
     att = mk<R>(1, 1, 1);
@@ -280,7 +284,7 @@ RT_HD bool shade_segment(const SceneView<R>& sc, const Closest<R>& c, V3<R>& o, 
             L = mk(T.x * m.c[0], T.y * m.c[1], T.z * m.c[2]);                 // emission
         } else {
             V3<R> nd, att;
-            if (scatter(m, h, unit, p, g, nd, att)) {
+            if (scatter<R, (FEAT & F_TRIS) != 0 && FEAT != F_ALL>(m, h, unit, p, g, nd, att)) {
                 T = mk(T.x * att.x, T.y * att.y, T.z * att.z);
                 o = h.p;
                 d = nd;
