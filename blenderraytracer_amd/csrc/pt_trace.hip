@@ -274,6 +274,18 @@ constexpr bool parks() { return RT_PARK != 0 && sizeof(R) == 8 && uses_stack<ACC
 #ifndef RT_DEFER_REGEN
 #define RT_DEFER_REGEN 16
 #endif
+// Scenes with triangles take a higher threshold in every kernel (mesh50k 256 spp, lean tree kernel: K = 8 /
+// 16 / 24 / 32 / 40 / 48 / 56: 7,503 / 7,579 / 7,609 / 7,611 / 7,621 / 7,544 / 7,464 Msamples/s,
+// interleaved; their walks are long, so fewer, fuller regenerations pay).  One threshold per scene, in
+// every kernel, keeps the per-pixel summation order — and so BVH == brute force bit for bit — kernel-
+// independent (a wave's schedule depends on its items, its segments and K only).
+#ifndef RT_DEFER_REGEN_TRI
+#define RT_DEFER_REGEN_TRI 40
+#endif
+template <class R>
+__device__ __forceinline__ int defer_regen(const SceneView<R>& sc) {
+    return sc.num_tri_nodes > 0 ? RT_DEFER_REGEN_TRI : RT_DEFER_REGEN;
+}
 
 // CANCEL: the launch carries a cancel word (progressive renders, Counters::cancel); the instantiation
 // without it holds no polling code (the poll's code alone cost 1.4 % on RTOW)
@@ -350,6 +362,7 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
         start_sample<R, false, feat_of<ACC>()>(sc, im, i, j, pkey, s, g, o, d);
     };
     uint32_t next = 64;                       // items [0, 64) are dealt to lanes 0..63 up front
+    const int defer_k = defer_regen(sc);     // RT_DEFER_REGEN (wave-uniform)
     bool live = (uint32_t)lane < total;
     if (live) begin_item((uint32_t)lane);
     bool waiting = false;                     // the lane's sample is done, its next not yet started
@@ -392,7 +405,7 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
         }
         const uint64_t t2 = RT_TICK();
         const uint64_t need = __ballot(waiting);
-        if (need && (__popcll(need) >= RT_DEFER_REGEN || __ballot(!waiting) == 0)) {
+        if (need && (__popcll(need) >= defer_k || __ballot(!waiting) == 0)) {
             if (waiting) {
                 const uint32_t k = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0));
@@ -476,6 +489,7 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
         start_sample<R, sizeof(R) == 4 || (RT_CAM_RELOAD_LEAN64 != 0 && ACC == ACC_GRID_LDS_LEAN), feat_of<ACC>()>(sc, im, i, j, pkey, s, g, o, d);
     };
     uint32_t next = 64;                       // items [0, 64) are dealt to lanes 0..63 up front
+    const int defer_k = defer_regen(sc);     // RT_DEFER_REGEN (wave-uniform)
     bool live = (uint32_t)lane < total;
     if (live) begin_item((uint32_t)lane);
     bool waiting = false;                     // as trace_pool_kernel (RT_DEFER_REGEN)
@@ -502,7 +516,7 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
         }
         const uint64_t t2 = RT_TICK();
         const uint64_t need = __ballot(waiting);
-        if (need && (__popcll(need) >= RT_DEFER_REGEN || __ballot(!waiting) == 0)) {
+        if (need && (__popcll(need) >= defer_k || __ballot(!waiting) == 0)) {
             if (waiting) {
                 const uint32_t k = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0));
