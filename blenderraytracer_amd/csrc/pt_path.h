@@ -300,6 +300,16 @@ RT_HD bool shade_segment(const SceneView<R>& sc, const Closest<R>& c, V3<R>& o, 
 }
 
 // Trace samples [im.s_begin, s_end) of crop pixel (cx, cy), adding radiance into sum[0..2].
+// In binary64 with maxBounces <= RT_REC_DEPTH, a sample's radiance is evaluated in the order of the
+// reference's recursion (ray-tracer.js:102-121: emitted + attenuation * rayColor(scattered)): the
+// attenuations are kept and multiplied onto the path's end value from the last bounce back, a0 * (a1 *
+// (... * X)), where the sample pool carries the throughput forward, ((a0 * a1) * ...) * X.  emitted is
+// zero for every material that scatters (an Emissive hit ends the path), so this is the recursion's
+// value bit for bit; with the samples added in sample order (this function) the means are the
+// reference's.  Deeper renders carry the throughput forward.
+#ifndef RT_REC_DEPTH
+#define RT_REC_DEPTH 16
+#endif
 template <class R, bool COUNT, int ACC = ACC_BRUTE>
 RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int cx, int cy, int s_end, double* sum,
                               BvhStack stk = BvhStack{nullptr, 0}) {
@@ -311,6 +321,9 @@ RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int
     Rng<R> g;
     V3<R> o, d, T = mk<R>(1, 1, 1);
     int depth = im.max_depth;
+    const bool rec = sizeof(R) == 8 && im.max_depth <= RT_REC_DEPTH;
+    V3<R> att[RT_REC_DEPTH];                   // rec: the sample's attenuations, bounce by bounce
+    int nb = 0;
     if (s < s_end) start_sample(sc, im, i, j, pkey, s, g, o, d);
     while (s < s_end) {
         const uint64_t t0 = RT_TICK();
@@ -319,10 +332,16 @@ RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int
         if (RT_PROFILE) res.cyc[0] += t1 - t0;
         ++res.segments;
         V3<R> L;
+        if (rec) T = mk<R>(1, 1, 1);           // then T = 1 * attenuation and L = 1 * X: exact
         const bool done = shade_segment(sc, c, o, d, T, depth, g, L);
         const uint64_t t2 = RT_TICK();
         if (RT_PROFILE) res.cyc[1] += t2 - t1;
+        if (rec && !done) att[nb++] = T;
         if (done) {
+            if (rec) {
+                for (int k = nb - 1; k >= 0; --k) L = mk(att[k].x * L.x, att[k].y * L.y, att[k].z * L.z);
+                nb = 0;
+            }
             sx += (double)L.x; sy += (double)L.y; sz += (double)L.z;
             if (COUNT) res.draws += g.k;
             ++s;

@@ -50,15 +50,13 @@ def test_f64_matches_reference(gpu, case):
 
 
 @pytest.mark.parametrize("case", gc.case_names())
-def test_f64_sample_order_ulps_from_reference(gpu, case):
+def test_f64_sample_order_bit_exact_to_reference(gpu, case):
     """In the reference's own summation order (rt_settings.sum_order = RT_SUM_SAMPLE_ORDER: each pixel's
-    samples added in sample order, ray-tracer.js:202-206) the GPU's binary64 render differs from the
-    reference only by the association of each path's products: the kernel carries the throughput forward
-    (T *= attenuation per bounce) where the reference's recursive rayColor multiplies on the way back
-    (attenuation * rayColor(scattered), materials.js / ray-tracer.js:165-180).  Everything else — every
-    decision, Math.pow / exp / sin / cos (V8's own algorithms, csrc/js_math.h), the sums' order — is the
-    reference's, so the means lie within a few ulps (asserted: 8; measured at most 3, 90-100 % of channels
-    bit-identical, configs 3 and 5 fully) and the RGBA8 bytes are identical."""
+    samples added in sample order, ray-tracer.js:202-206) the GPU's binary64 render IS the reference's,
+    bit for bit: every decision, Math.pow / exp / sin / cos (V8's own algorithms, csrc/js_math.h) and each
+    sample's radiance in the recursion's order (pt_path.h trace_pixel: a0 * (a1 * (... * X)), as
+    rayColor's emitted + attenuation * rayColor(scattered)).  Means, post-gamma values (float32 storage),
+    RGBA8 bytes and the denoised frame equal the fixtures exactly."""
     rt, c = gc.tracer_for(case, precision=capi.RT_PREC_F64)
     rt.sum_order = capi.RT_SUM_SAMPLE_ORDER
     r = rt.render(crop=c["crop"], want=WANT)
@@ -68,8 +66,12 @@ def test_f64_sample_order_ulps_from_reference(gpu, case):
     a, b = r["mean"][~nan], lin[~nan]
     ulps = np.abs(a - b) / np.spacing(np.maximum(np.abs(b), 2.0 ** -1022))
     print(f"{case}: {np.mean(a == b):.4f} of channels bit-identical, max {ulps.max(initial=0):.1f} ulps")
-    assert np.all(ulps <= 8)
+    assert np.array_equal(a, b)
     assert np.array_equal(r["rgba8"], gc.load_array(case, "rgba8"))
+    ref_post = gc.load_array(case, "denoised")[..., :3] if gc.has(case, "denoised") else gc.load_array(case, "post")
+    ok = ~np.isnan(ref_post)
+    assert np.array_equal(np.isnan(r["post"][..., :3]), ~ok)
+    assert np.array_equal(r["post"][..., :3][ok], ref_post.astype(np.float32)[ok])
     rt.close()
 
 
