@@ -23,8 +23,10 @@ def build(defines=(), name="libpt_hostcheck.so"):
     if os.path.exists(target) and all(os.path.getmtime(target) >= os.path.getmtime(d) for d in DEPS):
         return target
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    tmp = "%s.tmp%d" % (target, os.getpid())     # parallel test workers: build aside, rename atomically
     subprocess.check_call([hipcc, "--offload-host-only", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-                           *[f"-D{d}" for d in defines], "-I", os.path.join(ROOT, "include"), SRC, "-o", target])
+                           *[f"-D{d}" for d in defines], "-I", os.path.join(ROOT, "include"), SRC, "-o", tmp])
+    os.replace(tmp, target)
     return target
 
 

@@ -24,7 +24,9 @@ BIN = os.path.join(HERE, "hostcheck", "_build", "queue_slots_check")
 def checker():
     os.makedirs(os.path.dirname(BIN), exist_ok=True)
     if not os.path.exists(BIN) or any(os.path.getmtime(BIN) < os.path.getmtime(p) for p in (SRC, HDR)):
-        subprocess.check_call(["g++", "-O2", "-std=c++17", "-pthread", "-Wall", SRC, "-o", BIN])
+        tmp = "%s.tmp%d" % (BIN, os.getpid())    # parallel test workers: build aside, rename atomically
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-pthread", "-Wall", SRC, "-o", tmp])
+        os.replace(tmp, BIN)
     return BIN
 
 
