@@ -291,6 +291,10 @@ struct SceneView {
     int num_grid_cells;            // 0: no grid
     int num_grid_recs;             // grid_cell[num_grid_cells]: registrations (records in grid_leaf)
     int use_grid;                  // choose_walk (scene_pack.h): the trace kernel walks the grid
+    // tri_exit_bound (binary64): per triangle id {C+, C-}, upper bounds of n.x and -n.x over every vertex
+    // of every triangle (+inf: not computed / no use), and the bound's scene constants
+    const double* tri_exit;
+    double exit_k0, exit_k1, exit_k2, exit_l1, exit_l2;
     // camera (camera.js:8-36 vectors, computed on the host in binary64)
     R cam_o[3], cam_llc[3], cam_h[3], cam_v[3], cam_u[3], cam_vv[3], cam_w[3];   // contiguous with
     R lens_radius;                                                                 // lens_radius: start_sample
@@ -301,6 +305,47 @@ struct SceneView {
 };
 
 enum HitKind : int { HIT_NONE = -1, HIT_SPHERE = 0, HIT_PLANE = 1, HIT_BOX = 2, HIT_TRI = 3 };
+
+// tri_exit_bound.  A ray leaving triangle A's plane on the side away from every triangle of the scene
+// cannot hit a triangle, so its segment skips the triangle walk (a convex mesh's reflected rays: config 5).
+// N = +-n (n: A's stored normal, |n|_2 within 1e-6 of 1, else C = +inf), C >= N.w over the exact vertices w
+// in {v0, v0 + e1, v0 + e2} of every triangle (scene_pack.h build_tri_exit), g = N.d >= 0, a = N.o.  Take
+// eps = 2^-53, Me >= every |e1|inf, |e2|inf, Mv >= every |v0|inf, md = |d|inf, mo = |o|inf, Ms = mo + Mv.
+// The binary64 test (triangle_candidate) decides through A = d.(e2 x e1)..., X, Y, Z (tri_filter_bound),
+// computed within EA = 64 eps md Me^2, EX = EY = 64 eps md Me Ms, EZ = 64 eps Me^2 Ms of the exact values.
+// Suppose it accepts a triangle f at t64 >= 0.001 with L1: 1e4 (EX + 1.01 EA) <= 0.004 and L2: EZ <= 1e-9.
+//  - |A64| >= 1e-4, so |A| > 0 and |A - A64| / |A64| <= 1e4 EA <= 0.004;
+//  - the exact u = X / A, v = Y / A lie within du = 2.1 eps + 1e4 (EX + 1.01 EA) of u64, v64 (in [0, 1]),
+//    so the weights (1 - u - v, u, v) of the exact ray point x(t) = v0 + u e1 + v e2 are >= -delta,
+//    delta = eps + 2 du, and N.x(t) <= C + 2 delta |N|_1 2 Me <= C + 7 delta Me;
+//  - the exact t = Z / A >= (0.001 (1 - 2.1 eps) - 1e4 EZ) / (1 + 1e4 EA) >= 0.000986 > T0 = 0.00095;
+//  - but N.x(t) = a + t g >= a + T0 g.
+// So no triangle is accepted when a - C + T0 g > 7 delta Me + the evaluation errors of a, g and the sum
+// (<= eps (10.6 mo + 5.3 Mv + 5.3 Me + 0.01 md)): the check below is twice that total,
+//   B = K0 + K1 md (mo + K2) + 24 eps (mo + md),  K0 = 2 eps (42 Me + 12 Mv),  K1 = 2 eps 8.96e6 Me^2,
+//   K2 = Mv + 1.01 Me,
+// and L1, L2 as md (mo + K2) <= exit_l1, mo <= exit_l2.  NaN anywhere fails a comparison: no skip.
+// tests/test_tri_exit.py: grazing and adversarial exits checked against the binary64 test of every triangle.
+#ifndef RT_TRI_EXIT
+#define RT_TRI_EXIT 1
+#endif
+template <class R>
+RT_HD bool leaves_tri_hull(const SceneView<R>& sc, int id, V3<R> o, V3<R> d) {
+    if constexpr (sizeof(R) != 8 || RT_TRI_EXIT == 0) return false;
+    else {
+        const TriRec<R>& tr = sc.tris[id];
+        const double gp = tr.nx * d.x + tr.ny * d.y + tr.nz * d.z;
+        const double an = tr.nx * o.x + tr.ny * o.y + tr.nz * o.z;
+        const bool pos = gp > 0.0;
+        const double C = sc.tri_exit[2 * id + (pos ? 0 : 1)];
+        const double g = pos ? gp : -gp, a = pos ? an : -an;
+        const double mo = fmax(fabs(o.x), fmax(fabs(o.y), fabs(o.z)));
+        const double md = fmax(fabs(d.x), fmax(fabs(d.y), fabs(d.z)));
+        const double mm = md * (mo + sc.exit_k2);
+        const double bnd = sc.exit_k0 + sc.exit_k1 * mm + 0x1.8p-49 * (mo + md);      // 24 eps = 3 * 2^-50
+        return mm <= sc.exit_l1 && mo <= sc.exit_l2 && (a - C) + 0.00095 * g > bnd;
+    }
+}
 
 template <class R>
 struct Closest { R t; int kind, idx, mat, obj; };   // obj: World.objects index (BVH mode only)
@@ -1004,7 +1049,7 @@ RT_HD void tri_leaf_filtered(const SceneView<R>& sc, int fc, const TriRay& tr, V
 // LDSN: the sphere tree's nodes are read from their LDS copy in stk (ACC_BVH_SPHERES_LDS).
 // TLDS: the triangle tree's top levels are read from their LDS copy in stk (ACC_BVH_TRI_LDS).
 template <class R, bool WIDE, bool TRI = true, bool LDSN = false, bool TLDS = false, int FEAT = F_ALL>
-RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
+RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk, bool skip_tri = false) {
     const R tmin = (R)0.001;
     Closest<R> b{(R)INFINITY, HIT_NONE, 0, 0, -1};
     brute_planes_boxes<R, FEAT>(sc, o, d, tmin, b);
@@ -1020,7 +1065,7 @@ RT_HD Closest<R> closest_hit_bvh(const SceneView<R>& sc, V3<R> o, V3<R> d, Work&
         if (sc.num_sphere_nodes > 0)
             bvh_walk<WIDE, LDSN ? 1 : 0>(sc.sphere_nodes, sc.num_sphere_nodes, sc.sphere_wide, br, tl, stk, w, leaf);
     }
-    if (TRI && sc.num_tri_nodes > 0) {
+    if (TRI && sc.num_tri_nodes > 0 && !skip_tri) {
         if constexpr (sizeof(R) == 8 && RT_TRI_FILTER != 0) {
             const TriRay tr = make_tri_ray(o, d);
             auto leaf = [&](int fc) { tri_leaf_filtered(sc, fc, tr, o, d, tmin, b, tl, w); };
@@ -1262,25 +1307,25 @@ template <class R, int ACC> constexpr bool sc_reload() {
 }
 // LOCAL: sc is closest_hit_acc's own reloaded copy
 template <class R, int ACC, bool LOCAL = false>
-RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk) {
+RT_HD Closest<R> closest_hit_acc(const SceneView<R>& sc, V3<R> o, V3<R> d, Work& w, BvhStack stk, bool skip_tri = false) {
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (!LOCAL && sc_reload<R, ACC>()) {
         typedef const __attribute__((address_space(4))) SceneView<R>* SvPtr;
         SvPtr p = (SvPtr)__builtin_amdgcn_kernarg_segment_ptr();
         asm volatile("" : "+s"(p));
         const SceneView<R> scl = *p;
-        return closest_hit_acc<R, ACC, true>(scl, o, d, w, stk);
+        return closest_hit_acc<R, ACC, true>(scl, o, d, w, stk, skip_tri);
     }
 #endif
-    if constexpr (ACC == ACC_BVH) return closest_hit_bvh<R, false>(sc, o, d, w, stk);
-    else if constexpr (ACC == ACC_BVH_STACK) return closest_hit_bvh<R, true>(sc, o, d, w, stk);
+    if constexpr (ACC == ACC_BVH) return closest_hit_bvh<R, false>(sc, o, d, w, stk, skip_tri);
+    else if constexpr (ACC == ACC_BVH_STACK) return closest_hit_bvh<R, true>(sc, o, d, w, stk, skip_tri);
     else if constexpr (ACC == ACC_BVH_SPHERES) return closest_hit_bvh<R, true, false>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_BVH_SPHERES_LDS) return closest_hit_bvh<R, true, false, true>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_GRID) return closest_hit_grid<R>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_GRID_LDS) return closest_hit_grid<R, true>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_GRID_LDS_LEAN) return closest_hit_grid<R, true, feat_of<ACC>(), LOCAL>(sc, o, d, w, stk);
     else if constexpr (ACC == ACC_BVH_STACK_LEAN)
-        return closest_hit_bvh<R, true, true, false, false, feat_of<ACC>()>(sc, o, d, w, stk);
+        return closest_hit_bvh<R, true, true, false, false, feat_of<ACC>()>(sc, o, d, w, stk, skip_tri);
     else if constexpr (ACC == ACC_BVH_TRI_LDS) return closest_hit_bvh<R, true, true, false, true>(sc, o, d, w, stk);
     else return closest_hit_runs<R, feat_of<ACC>()>(sc, o, d);
 }

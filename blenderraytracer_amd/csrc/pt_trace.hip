@@ -366,6 +366,7 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
     bool live = (uint32_t)lane < total;
     if (live) begin_item((uint32_t)lane);
     bool waiting = false;                     // the lane's sample is done, its next not yet started
+    bool skip_tri = false;
     while (live) {                            // lanes only ever leave this loop, so every live lane
         const uint64_t t0 = RT_TICK();        // has seen every update of `next`
         if (!waiting) {
@@ -374,7 +375,7 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
                 park_i[0] = (uint32_t)depth; park_i[64] = isegs; park_i[128] = m;
                 park_i[192] = g.key; park_i[256] = g.k; park_i[320] = res.segments;
             }
-            const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, res.work, stk);
+            const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, res.work, stk, skip_tri);
             if constexpr (PARK) {
                 // the walk's stack stores may alias these slots as far as the compiler can tell: the
                 // values are reloaded, not forwarded, so their registers are free during the walk
@@ -389,6 +390,10 @@ void trace_pool_kernel(const TraceArgs<R> args, double* __restrict__ part, const
             ++isegs;
             V3<R> L;
             waiting = shade_segment<R, feat_of<ACC>()>(sc, c, o, d, T, depth, g, L);
+            // the next segment leaves the triangle just hit away from every triangle: no triangle walk
+            // (tri_exit_bound, pt_core.h; binary64 only)
+            if constexpr (sizeof(R) == 8 && (ACC == ACC_BVH || ACC == ACC_BVH_STACK || ACC == ACC_BVH_STACK_LEAN))
+                skip_tri = !waiting && c.kind == HIT_TRI && leaves_tri_hull(sc, c.idx, o, d);
             if (RT_PROFILE) res.cyc[1] += RT_TICK() - t1;
             if (waiting) {
                 if (COUNT) {

@@ -101,6 +101,7 @@ struct DeviceScene {
     DevBuf<SphereLeaf<R>> bvh_sphere_leaf;
     DevBuf<TriLeaf<R>> bvh_tri_leaf;
     DevBuf<TriFilter> tri_filter;
+    DevBuf<double> tri_exit;
     DevBuf<SphereLeaf<R>> big_sphere_leaf;
     DevBuf<Bvh2Node> sphere_wide, tri_wide;
     DevBuf<int> grid_cell;
@@ -110,7 +111,7 @@ struct DeviceScene {
         runs.release(); spheres.release(); sphere_filter.release(); sphere_r.release(); sphere_inv_r.release(); planes.release(); boxes.release(); tris.release();
         sphere_mat.release(); plane_mat.release(); box_mat.release(); tri_mat.release(); perm.release(); mats.release();
         plane_obj.release(); box_obj.release(); sphere_nodes.release(); tri_nodes.release(); bvh_sphere_leaf.release();
-        bvh_tri_leaf.release(); tri_filter.release(); big_sphere_leaf.release();
+        bvh_tri_leaf.release(); tri_filter.release(); tri_exit.release(); big_sphere_leaf.release();
         sphere_wide.release(); tri_wide.release(); grid_cell.release(); grid_leaf.release();
     }
 };
@@ -126,7 +127,7 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     UP(box_mat, hs.box_mat); UP(tri_mat, hs.tri_mat); UP(perm, rec.perm); UP(mats, rec.mats);
     UP(plane_obj, hs.plane_obj); UP(box_obj, hs.box_obj); UP(sphere_nodes, hs.sphere_bvh); UP(tri_nodes, hs.tri_bvh);
     UP(bvh_sphere_leaf, rec.bvh_sphere_leaf); UP(bvh_tri_leaf, rec.bvh_tri_leaf); UP(tri_filter, rec.tri_filter); UP(big_sphere_leaf, rec.big_sphere_leaf); UP(sphere_wide, hs.sphere_wide); UP(tri_wide, hs.tri_wide);
-    UP(grid_cell, hs.grid_cell); UP(grid_leaf, rec.grid_leaf);
+    UP(grid_cell, hs.grid_cell); UP(grid_leaf, rec.grid_leaf); UP(tri_exit, hs.tri_exit);
 #undef UP
     if (e != hipSuccess) return fail(RT_ERR_DEVICE, "scene upload: %s", hipGetErrorString(e));
     SceneView<R>& v = ds.view;
@@ -136,6 +137,7 @@ int build_device(DeviceScene<R>& ds, const HostScene& hs, const rt_scene_desc& d
     v.tri_mat = ds.tri_mat.p; v.mats = ds.mats.p; v.perm = ds.perm.p;
     v.plane_obj = ds.plane_obj.p; v.box_obj = ds.box_obj.p; v.sphere_nodes = ds.sphere_nodes.p; v.tri_nodes = ds.tri_nodes.p;
     v.bvh_sphere_leaf = ds.bvh_sphere_leaf.p; v.bvh_tri_leaf = ds.bvh_tri_leaf.p; v.tri_filter = ds.tri_filter.p;
+    v.tri_exit = ds.tri_exit.p;
     v.big_spheres = ds.big_sphere_leaf.p;
     v.sphere_wide = ds.sphere_wide.p; v.tri_wide = ds.tri_wide.p;
     v.grid_cell = ds.grid_cell.p; v.grid_leaf = ds.grid_leaf.p;

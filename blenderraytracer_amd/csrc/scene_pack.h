@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt_hip.h"
@@ -34,6 +35,9 @@ struct HostScene {   // precision-independent staging, binary64 as packed by the
     int bvh_depth = 0;                                            // deepest leaf of either tree
     int num_prims = 0;
     double record_bytes = 0;      // SURVEY §8d canonical bytes tested per segment
+    // build_tri_exit (pt_core.h tri_exit_bound): {C+, C-} per triangle and the bound's constants
+    std::vector<double> tri_exit;
+    double exit_k0 = 0, exit_k1 = 0, exit_k2 = 0, exit_l1 = -1, exit_l2 = -1;
 };
 
 inline bool pack_host(const rt_scene_desc& d, HostScene& hs, std::string& err) {
@@ -491,6 +495,85 @@ inline void build_grid(HostScene& hs, const std::vector<BuildPrim>& prims) {
     }
 }
 
+// tri_exit_bound (pt_core.h): for every triangle A and each side N = +-n of its stored normal n, an upper
+// bound C of N.w over the exact vertices w in {v0, v0 + e1, v0 + e2} of every triangle, found by a
+// branch-and-bound walk of the triangle tree: a subtree is skipped when the support of its box,
+// sum_k max(N_k lo_k, N_k hi_k) + 2^-17 max|box| (the box's own rounding and the exact vertices' offsets from
+// the given ones), is below the best value so far.  A side gets C = +inf when some vertex lies more than
+// 0.002 in front of A's own vertices (no exit ray, |d|_2 <= 2, could then pass the check: the walk stops
+// there), when |n|_2 is not within 1e-6 of 1, or when any triangle has a non-finite coordinate.  The visited
+// values carry the rounding pad 16 eps (Mv + Me) + 4 eps |C|.
+#ifndef RT_TRI_EXIT_MAX
+#define RT_TRI_EXIT_MAX (1 << 23)        // triangles; larger scenes skip the bounds (every C = +inf)
+#endif
+inline void build_tri_exit(HostScene& hs) {
+    const size_t T = hs.tri_mat.size();
+    hs.tri_exit.assign(2 * T, INFINITY);
+    hs.exit_l1 = hs.exit_l2 = -1;       // no exit ray passes
+    if (T == 0 || T > (size_t)RT_TRI_EXIT_MAX || hs.tri_bvh.empty()) return;
+    double Mv = 0, Me = 0;
+    for (size_t i = 0; i < T; ++i) {
+        const double* t = &hs.tris[12 * i];
+        for (int k = 0; k < 9; ++k)
+            if (!std::isfinite(t[k])) return;
+        for (int k = 0; k < 3; ++k) {
+            Mv = std::max(Mv, std::fabs(t[k]));
+            Me = std::max(Me, std::max(std::fabs(t[3 + k]), std::fabs(t[6 + k])));
+        }
+    }
+    if (!(Me > 0) || !(Me < 1e100) || !(Mv < 1e100)) return;
+    const double eps = 0x1p-53;
+    hs.exit_k0 = 2 * eps * (42 * Me + 12 * Mv);
+    hs.exit_k1 = 2 * eps * 8.96e6 * Me * Me;
+    hs.exit_k2 = Mv + 1.01 * Me;
+    hs.exit_l1 = 0.99 * (0.004 / (1e4 * 64 * eps * Me));          // L1: 1e4 (EX + 1.01 EA) <= 0.004
+    hs.exit_l2 = 0.99 * (1e-9 / (64 * eps * Me * Me)) - Mv;       // L2: EZ <= 1e-9
+    const double pad = 16 * eps * (Mv + Me);
+    const BvhNode* nodes = hs.tri_bvh.data();
+    const int count = (int)hs.tri_bvh.size();
+    auto side = [&](const double* A, const double N[3]) -> double {
+        auto phi3 = [&](const double* t, double& mx) {
+            const double p0 = N[0] * t[0] + N[1] * t[1] + N[2] * t[2];
+            const double p1 = p0 + (N[0] * t[3] + N[1] * t[4] + N[2] * t[5]);
+            const double p2 = p0 + (N[0] * t[6] + N[1] * t[7] + N[2] * t[8]);
+            mx = std::max(mx, std::max(p0, std::max(p1, p2)));
+        };
+        double best = -INFINITY;
+        phi3(A, best);
+        const double stop = best + 0.002;
+        int ni = 0;
+        while (ni < count) {
+            const BvhNode& n = nodes[ni];
+            double sup = 0, mb = 0;
+            for (int k = 0; k < 3; ++k) {
+                sup += std::max(N[k] * (double)n.lo[k], N[k] * (double)n.hi[k]);
+                mb = std::max(mb, std::max(std::fabs((double)n.lo[k]), std::fabs((double)n.hi[k])));
+            }
+            if (sup + 0x1p-17 * mb <= best) { ni = n.skip; continue; }
+            if (n.fc == 0) { ++ni; continue; }
+            for (int k = n.fc >> 4, e = k + (n.fc & 15); k < e; ++k) phi3(&hs.tris[12 * (size_t)hs.tri_bvh_prims[k]], best);
+            if (!(best <= stop)) return INFINITY;
+            ni = n.skip;
+        }
+        return best + (pad + 4 * eps * std::fabs(best));
+    };
+    auto work = [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; ++i) {
+            const double* t = &hs.tris[12 * i];
+            const double nn = t[9] * t[9] + t[10] * t[10] + t[11] * t[11];
+            if (!(std::fabs(nn - 1.0) <= 1e-6)) continue;              // |n|_2 within 5e-7 of 1
+            const double np[3] = {t[9], t[10], t[11]}, nm[3] = {-t[9], -t[10], -t[11]};
+            hs.tri_exit[2 * i] = side(t, np);
+            hs.tri_exit[2 * i + 1] = side(t, nm);
+        }
+    };
+    const size_t nt = std::min<size_t>(16, std::max(1u, std::thread::hardware_concurrency()));
+    if (T < 4096 || nt == 1) { work(0, T); return; }
+    std::vector<std::thread> th;
+    for (size_t w = 0; w < nt; ++w) th.emplace_back(work, T * w / nt, T * (w + 1) / nt);
+    for (auto& x : th) x.join();
+}
+
 inline void build_bvhs(HostScene& hs) {
     BvhBuilder sb;
     sb.kLeafMax = RT_BVH_SPHERE_LEAF;
@@ -528,6 +611,7 @@ inline void build_bvhs(HostScene& hs) {
     hs.tri_bvh_prims = std::move(tb.order);
     hs.sphere_wide = make_wide(hs.sphere_bvh);
     hs.tri_wide = make_wide(hs.tri_bvh, RT_TRI_TOP_NODES);
+    build_tri_exit(hs);
 }
 
 // The binary32 pre-filter record of a triangle {v0, e1, e2, ...} (binary64, pt_core.h tri_filter_bound):
@@ -678,6 +762,8 @@ void fill_view_constants(SceneView<R>& v, const HostScene& hs, const rt_scene_de
     v.grid_far = hs.grid_far;
     v.use_grid = hs.use_grid ? 1 : 0;
     v.stack_entries = std::max(1, hs.bvh_depth);
+    v.exit_k0 = hs.exit_k0; v.exit_k1 = hs.exit_k1; v.exit_k2 = hs.exit_k2;
+    v.exit_l1 = hs.exit_l1; v.exit_l2 = hs.exit_l2;
     const rt_camera_desc& c = d.camera;
     for (int k = 0; k < 3; ++k) {
         v.cam_o[k] = (R)c.origin[k];
@@ -722,7 +808,7 @@ inline SceneView<double> host_view(const HostScene& hs, const rt_scene_desc& d, 
     v.plane_obj = hs.plane_obj.data(); v.box_obj = hs.box_obj.data();
     v.sphere_nodes = hs.sphere_bvh.data(); v.tri_nodes = hs.tri_bvh.data();
     v.bvh_sphere_leaf = rec.bvh_sphere_leaf.data(); v.bvh_tri_leaf = rec.bvh_tri_leaf.data();
-    v.tri_filter = rec.tri_filter.data();
+    v.tri_filter = rec.tri_filter.data(); v.tri_exit = hs.tri_exit.data();
     v.big_spheres = rec.big_sphere_leaf.data();
     v.sphere_wide = hs.sphere_wide.data(); v.tri_wide = hs.tri_wide.data();
     v.grid_cell = hs.grid_cell.data(); v.grid_leaf = rec.grid_leaf.data();

@@ -30,7 +30,7 @@ struct HostView {
         v.plane_obj = hs.plane_obj.data(); v.box_obj = hs.box_obj.data();
         v.sphere_nodes = hs.sphere_bvh.data(); v.tri_nodes = hs.tri_bvh.data();
         v.bvh_sphere_leaf = rec.bvh_sphere_leaf.data(); v.bvh_tri_leaf = rec.bvh_tri_leaf.data();
-        v.tri_filter = rec.tri_filter.data();
+        v.tri_filter = rec.tri_filter.data(); v.tri_exit = hs.tri_exit.data();
         v.big_spheres = rec.big_sphere_leaf.data();
         v.sphere_wide = hs.sphere_wide.data(); v.tri_wide = hs.tri_wide.data();
         v.grid_cell = hs.grid_cell.data(); v.grid_leaf = rec.grid_leaf.data();
