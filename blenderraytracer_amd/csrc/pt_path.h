@@ -324,16 +324,19 @@ RT_HD PixelResult trace_pixel(const SceneView<R>& sc, const ImageParams& im, int
     const bool rec = sizeof(R) == 8 && im.max_depth <= RT_REC_DEPTH;
     V3<R> att[RT_REC_DEPTH];                   // rec: the sample's attenuations, bounce by bounce
     int nb = 0;
+    bool skip_tri = false;                     // tri_exit_bound (pt_core.h)
     if (s < s_end) start_sample(sc, im, i, j, pkey, s, g, o, d);
     while (s < s_end) {
         const uint64_t t0 = RT_TICK();
-        const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, res.work, stk);
+        const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, res.work, stk, skip_tri);
         const uint64_t t1 = RT_TICK();
         if (RT_PROFILE) res.cyc[0] += t1 - t0;
         ++res.segments;
         V3<R> L;
         if (rec) T = mk<R>(1, 1, 1);           // then T = 1 * attenuation and L = 1 * X: exact
         const bool done = shade_segment(sc, c, o, d, T, depth, g, L);
+        if constexpr (sizeof(R) == 8 && (ACC == ACC_BVH || ACC == ACC_BVH_STACK || ACC == ACC_BVH_STACK_LEAN))
+            skip_tri = !done && c.kind == HIT_TRI && leaves_tri_hull(sc, c.idx, o, d);
         const uint64_t t2 = RT_TICK();
         if (RT_PROFILE) res.cyc[1] += t2 - t1;
         if (rec && !done) att[nb++] = T;
