@@ -278,9 +278,11 @@ constexpr bool parks() { return RT_PARK != 0 && sizeof(R) == 8 && uses_stack<ACC
 // 16 / 24 / 32 / 40 / 48 / 56: 7,503 / 7,579 / 7,609 / 7,611 / 7,621 / 7,544 / 7,464 Msamples/s,
 // interleaved; their walks are long, so fewer, fuller regenerations pay).  One threshold per scene, in
 // every kernel, keeps the per-pixel summation order — and so BVH == brute force bit for bit — kernel-
-// independent (a wave's schedule depends on its items, its segments and K only).
+// independent (a wave's schedule depends on its items, its segments and K only).  Re-measured with the exit
+// skip (tri_exit_bound): K = 24 / 32 / 40 / 48 / 56: 64.85 / 64.30 / 64.60 / 64.08 / 65.6 ms (interleaved,
+// two sessions, mesh50k 256 spp): 48.
 #ifndef RT_DEFER_REGEN_TRI
-#define RT_DEFER_REGEN_TRI 40
+#define RT_DEFER_REGEN_TRI 48
 #endif
 template <class R>
 __device__ __forceinline__ int defer_regen(const SceneView<R>& sc) {
