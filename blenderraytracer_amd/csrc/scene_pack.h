@@ -570,7 +570,12 @@ inline void build_tri_exit(HostScene& hs) {
     const size_t nt = std::min<size_t>(16, std::max(1u, std::thread::hardware_concurrency()));
     if (T < 4096 || nt == 1) { work(0, T); return; }
     std::vector<std::thread> th;
-    for (size_t w = 0; w < nt; ++w) th.emplace_back(work, T * w / nt, T * (w + 1) / nt);
+    size_t started = 0;
+    try {
+        for (; started < nt; ++started) th.emplace_back(work, T * started / nt, T * (started + 1) / nt);
+    } catch (...) {               // no thread to be had: this thread takes the ranges not started
+    }
+    for (size_t w = started; w < nt; ++w) work(T * w / nt, T * (w + 1) / nt);
     for (auto& x : th) x.join();
 }
 
