@@ -333,6 +333,9 @@ template <class R>
 RT_HD bool leaves_tri_hull(const SceneView<R>& sc, int id, V3<R> o, V3<R> d) {
     if constexpr (sizeof(R) != 8 || RT_TRI_EXIT == 0) return false;
     else {
+#if !defined(__HIP_DEVICE_COMPILE__)
+        if (!sc.tri_exit) return false;         // a host view built without the bounds (the device's always has them)
+#endif
         const TriRec<R>& tr = sc.tris[id];
         const double gp = tr.nx * d.x + tr.ny * d.y + tr.nz * d.z;
         const double an = tr.nx * o.x + tr.ny * o.y + tr.nz * o.z;
