@@ -500,16 +500,19 @@ __device__ __forceinline__ void pool_item(const TraceArgs<R>& args, double* __re
     bool live = (uint32_t)lane < total;
     if (live) begin_item((uint32_t)lane);
     bool waiting = false;                     // as trace_pool_kernel (RT_DEFER_REGEN)
+    int origin = -1;                          // RT_ORIGIN_LEAVE: the sphere the next segment starts on
     while (live) {                            // lanes only ever leave this loop, so every live lane
         const uint64_t t0 = RT_TICK();        // has seen every update of `next`
         if (!waiting) {
-            const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, res.work, stk);
+            const Closest<R> c = closest_hit_acc<R, ACC>(sc, o, d, res.work, stk, false, origin);
             const uint64_t t1 = RT_TICK();
             if (RT_PROFILE) res.cyc[0] += t1 - t0;
             ++res.segments;
             ++isegs;
             V3<R> L;
             waiting = shade_segment<R, feat_of<ACC>()>(sc, c, o, d, T, depth, g, L, lmats);
+            if constexpr (RT_ORIGIN_LEAVE && sizeof(R) == 8 && ACC == ACC_GRID_LDS_LEAN)
+                origin = !waiting && c.kind == HIT_SPHERE ? c.idx : -1;
             if (RT_PROFILE) res.cyc[1] += RT_TICK() - t1;
             if (waiting) {
                 if (COUNT) {

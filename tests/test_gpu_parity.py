@@ -280,6 +280,23 @@ def test_bvh_bit_identical_to_brute_mesh50k(gpu, precision):
     rt.close()
 
 
+def test_exit_skip_bit_identical_on_mesh_silhouette(gpu):
+    """tri_exit_bound on the device: the tree kernel skips the triangle walk of segments leaving the mesh
+    (pt_core.h leaves_tri_hull), the brute-force World-order kernel never skips.  Over the UV sphere's
+    silhouette, where reflections leave the mesh at grazing angles, the two agree bit for bit."""
+    rt = GpuRayTracer(1920, 1080, seed=11, precision=capi.RT_PREC_F64)
+    assert rt.load_from_json(load_scene_json("mesh50k"))
+    rt.update_render_settings({"maxBounces": 5, "samples": 8})
+    crop = (1090, 470, 96, 96)                  # the sphere's right edge (its centre projects to 960, 540)
+    rt.accel = capi.RT_ACCEL_BVH
+    a = rt.render(crop=crop, want=WANT)
+    rt.accel = capi.RT_ACCEL_BRUTE
+    b = rt.render(crop=crop, want=WANT)
+    assert np.array_equal(a["segments"], b["segments"]) and np.array_equal(a["draws"], b["draws"])
+    assert np.array_equal(a["mean"], b["mean"], equal_nan=True)
+    rt.close()
+
+
 def test_resume_with_one_batch_left_is_bit_exact(gpu):
     """A resume whose remaining samples are a single batch (the render as a whole has several) takes
     that batch's chunks from the whole render's rule, as the uninterrupted render did: bit-identical.
