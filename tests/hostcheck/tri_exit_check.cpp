@@ -4,7 +4,8 @@
 // skip the triangle walk, the binary64 test (triangle_candidate) of EVERY triangle must reject the ray.
 // usage: tri_exit_check <mesh> <rays> <seed> [mutation]
 //   mesh: sphere (config 5's 176 x 142 UV sphere, radius 1.2), sphere_off (the same, off the origin),
-//         cube, torus (not convex), bowl (an open half sphere), grid (coplanar triangles)
+//         cube, torus (not convex), bowl (an open half sphere), grid (coplanar triangles), pair (a sphere and
+//         a cube beside it in one scene)
 //   mutation: 0 none; 1 C from A's own vertices only; 2 the sides' bounds swapped
 // prints: rays=.. skips=.. violations=.. hits_not_skipped=.. exit_faces=..
 #include <cstdio>
@@ -58,6 +59,15 @@ int main(int argc, char** argv) {
             p[1] = c[1] + 1.2 * std::cos(th);
             p[2] = c[2] + 1.2 * std::sin(th) * std::sin(ph);
         });
+    } else if (mesh == "pair") {          // the UV sphere and a cube beside it: bounds over both objects' vertices
+        grid_mesh(T, 88, 71, [&](double s, double t, double* p) {
+            const double th = t * pi, ph = s * 2 * pi;
+            p[0] = 1.2 * std::sin(th) * std::cos(ph); p[1] = 1.2 * std::cos(th); p[2] = 1.2 * std::sin(th) * std::sin(ph);
+        });
+        const double v[8][3] = {{2.5, -.5, -.5}, {3.5, -.5, -.5}, {3.5, .5, -.5}, {2.5, .5, -.5}, {2.5, -.5, .5}, {3.5, -.5, .5}, {3.5, .5, .5}, {2.5, .5, .5}};
+        const int f[12][3] = {{0, 2, 1}, {0, 3, 2}, {4, 5, 6}, {4, 6, 7}, {0, 1, 5}, {0, 5, 4},
+                              {3, 6, 2}, {3, 7, 6}, {0, 4, 7}, {0, 7, 3}, {1, 2, 6}, {1, 6, 5}};
+        for (auto& q : f) add_tri(T, v[q[0]], v[q[1]], v[q[2]]);
     } else if (mesh == "torus") {
         grid_mesh(T, 96, 48, [&](double s, double t, double* p) {
             const double a = s * 2 * pi, b = t * 2 * pi, r = 1.0 + 0.4 * std::cos(b);

@@ -40,7 +40,7 @@ def run(binary, mesh, rays, seed, mutation=0):
 
 
 @pytest.mark.parametrize("mesh,rays", [("sphere", 6000), ("sphere_off", 6000), ("cube", 20000), ("torus", 20000),
-                                       ("bowl", 8000), ("grid", 20000)])
+                                       ("bowl", 8000), ("grid", 20000), ("pair", 8000)])
 def test_skipped_segments_hit_no_triangle(checker, mesh, rays):
     r = run(checker, mesh, rays, 7)
     assert r["rays"] == rays
@@ -55,7 +55,7 @@ def test_convex_mesh_every_face_is_an_exit_face(checker):
     assert r["exit_faces"] >= 49984 - 2 * 176
 
 
-@pytest.mark.parametrize("mesh,mutation", [("torus", 1), ("bowl", 1), ("sphere_off", 1), ("sphere_off", 2)])
+@pytest.mark.parametrize("mesh,mutation", [("torus", 1), ("bowl", 1), ("sphere_off", 1), ("sphere_off", 2), ("pair", 1)])
 def test_checker_catches_wrong_bounds(checker, mesh, mutation):
     """Mutations: C from the face's own vertices only (1), the two sides' bounds swapped (2) — both skip
     segments that do hit a triangle, and the checker sees it."""
