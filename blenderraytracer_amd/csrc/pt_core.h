@@ -1026,9 +1026,12 @@ RT_HD void tri_leaf(const SceneView<R>& sc, int fc, V3<R> o, V3<R> d, R tmin, Cl
 // tri_filter_bound) into a mask of survivors, then the binary64 test over the survivors only, reading
 // their 80-B records — the mirror of the sphere survivor masks (RT_GRID_COMPACT).  Same decisions as
 // tri_leaf (the filter rejects only what the binary64 test rejects; `better` is a total order, so the
-// survivors' order does not matter).  0: every triangle through the binary64 test (A/B).
+// survivors' order does not matter).  0: every triangle through the binary64 test.
+// Round 5: +1.5 % on config 5.  Since the exit skip (tri_exit_bound) the walks left are the camera and
+// ground rays that reach the mesh, and the filter no longer pays: mesh50k 256 spp f64 kernel time 58.7–59.0
+// without it vs 59.4–59.8 ms (interleaved x2, identical images), so it is off by default (1: A/B).
 #ifndef RT_TRI_FILTER
-#define RT_TRI_FILTER 1
+#define RT_TRI_FILTER 0
 #endif
 template <class R>
 RT_HD void tri_leaf_filtered(const SceneView<R>& sc, int fc, const TriRay& tr, V3<R> o, V3<R> d, R tmin,

@@ -279,8 +279,8 @@ constexpr bool parks() { return RT_PARK != 0 && sizeof(R) == 8 && uses_stack<ACC
 // interleaved; their walks are long, so fewer, fuller regenerations pay).  One threshold per scene, in
 // every kernel, keeps the per-pixel summation order — and so BVH == brute force bit for bit — kernel-
 // independent (a wave's schedule depends on its items, its segments and K only).  Re-measured with the exit
-// skip (tri_exit_bound): K = 24 / 32 / 40 / 48 / 56: 64.85 / 64.30 / 64.60 / 64.08 / 65.6 ms (interleaved,
-// two sessions, mesh50k 256 spp): 48.
+// skip (tri_exit_bound), kernel time: K = 24 / 32 / 40 / 48: 60.02 / 59.83 / 60.15 / 59.70 ms; 40 / 48 / 56:
+// 59.85 / 59.50 / 60.00 ms (interleaved, two sessions, mesh50k 256 spp): 48.
 #ifndef RT_DEFER_REGEN_TRI
 #define RT_DEFER_REGEN_TRI 48
 #endif
