@@ -44,10 +44,6 @@ static_assert(offsetof(TraceArgs<double>, sc) == 0 && offsetof(TraceArgs<float>,
 #ifndef RT_BVH_WAVES_PER_SIMD
 #define RT_BVH_WAVES_PER_SIMD 4   // binary64 BVH walk: 128 VGPRs (measured 3/4/5 waves: 5405/5462/5092)
 #endif
-#ifndef RT_BVH_LEAN_WAVES
-#define RT_BVH_LEAN_WAVES 5       // binary64 lean tree kernel (config 5) since the exit skip and the pre-filter off:
-#endif                            // 5 / 4 waves 58.4-58.6 / 58.7-59.2 ms (interleaved x2, mesh50k 256 spp; round 6
-                                  // before them: 5 waves -11 %)
 #ifndef RT_BVH_WAVES_F32
 #define RT_BVH_WAVES_F32 5        // binary32 BVH walk: 96 VGPRs (measured 4/5/6 waves: 6070/6628/6542)
 #endif
@@ -96,7 +92,6 @@ constexpr int waves_per_simd() {
     if constexpr (ACC == ACC_BVH_SPHERES) return sizeof(R) == 8 ? RT_SPHERES_WAVES_PER_SIMD : RT_SPHERES_WAVES_F32;
     if constexpr (ACC == ACC_BVH_SPHERES_LDS) return sizeof(R) == 8 ? RT_LDS_OCC_F64 : RT_LDS_OCC_F32;
     if constexpr (ACC == ACC_BVH_TRI_LDS) return sizeof(R) == 8 ? RT_BVH_WAVES_PER_SIMD : RT_BVH_WAVES_F32;
-    if constexpr (ACC == ACC_BVH_STACK_LEAN) return sizeof(R) == 8 ? RT_BVH_LEAN_WAVES : RT_BVH_WAVES_F32;
     return ACC >= ACC_BVH ? (sizeof(R) == 8 ? RT_BVH_WAVES_PER_SIMD : RT_BVH_WAVES_F32) : RT_MIN_WAVES_PER_SIMD;
 }
 
